@@ -1,0 +1,94 @@
+"""ctypes binding of the C ABI in include/mvmatch.h (libmvmatch.so).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc,
+--offload-arch=gfx950) into ``bpc_baseline_amd/lib/libmvmatch.so``.  There is
+no fallback: if the library is missing or fails to load, importing the ops
+raises, so the product path can never silently run anything but the HIP
+kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libmvmatch.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "mvmatch.h")
+
+MVM_OK = 0
+MVM_MAX_CAMS = 8
+MVM_MAX_PAIRS = 28
+
+
+class MvmError(RuntimeError):
+    """A non-zero status returned by the C ABI."""
+
+    def __init__(self, fn: str, status: int, message: str):
+        super().__init__(f"{fn} failed with status {status}: {message}")
+        self.status = status
+
+
+_vp = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); kept in the order of include/mvmatch.h
+SIGNATURES = {
+    "mvm_version": (ctypes.c_char_p, []),
+    "mvm_last_error_string": (ctypes.c_char_p, []),
+    "mvm_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "mvm_pairwise_residual_argmin": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp,            # pts, cam_offs, F, pair_a (host), pair_b (host)
+        _i32, _i32, _i32, _i32,             # n_scenes, n_cams, n_pairs, max_rows
+        _vp, _vp, _vp, _vp, _vp,            # dist_offs, row_offs, dist, argmin, minval
+        _vp]),                              # stream
+    "mvm_pairwise_residual_f64": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp,
+        _i32, _i32, _i32, _i32,
+        _i64, _i64, _vp,                    # mat_stride, ld, e
+        _vp]),
+    "mvm_triplet_workspace_bytes": (_sz, [_i32, _i32]),
+    "mvm_triplet_cost_argmin": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
+        _vp, _vp, _vp, _vp, _vp,            # cube_offs, row_offs, cube, argmin, minval
+        _vp, _sz, _vp]),                    # workspace, workspace_bytes, stream
+}
+
+_lib = None
+
+
+def header_symbols() -> list:
+    """Function names declared in include/mvmatch.h (for the export test)."""
+    with open(HEADER_PATH) as fh:
+        text = fh.read()
+    return re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(mvm_[a-z_0-9]+)\s*\(", text, re.M)
+
+
+def load(path: str = LIB_PATH):
+    """Load libmvmatch.so once and attach the C signatures.  Raises if missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(
+            f"{path} not found: build the HIP library first "
+            "(python -c 'import __graft_entry__ as g; g.build()')")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(fn_name: str, status: int) -> None:
+    if status != MVM_OK:
+        msg = load().mvm_last_error_string().decode(errors="replace")
+        raise MvmError(fn_name, status, msg or load().mvm_status_string(status).decode())
+
+
+def version() -> str:
+    return load().mvm_version().decode()

@@ -1,0 +1,98 @@
+"""Camera parameters and fundamental matrices (host side).
+
+Mirrors ``bpc/inference/utils/camera_utils.py`` of the reference.  The
+fundamental matrix is O(1) per camera pair and stays on the host, as in the
+reference: only the O(n^2) residual work goes to the GPU.
+
+Precision follows the reference exactly (camera_utils.py:23-46): K is float32
+(load_camera_params :16), R and t arrive as float64 (``calc_pose_matrix`` puts
+them in ``np.eye(4)``, data_utils.py:383-387), the skew matrix is cast to
+float32 (:31-35), and the product is float64.  Because the bits depend on the
+host BLAS, the parity fixtures store F as an *input* of the matcher.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Dict, Iterable, Sequence
+
+import numpy as np
+
+__all__ = [
+    "load_camera_params",
+    "compute_fundamental_matrix",
+    "calc_pose_matrix",
+    "camera_pairs",
+    "fundamental_matrices",
+]
+
+
+def load_camera_params(scene_dir: str, cam_ids: Iterable[str]) -> Dict[str, Dict[str, dict]]:
+    """Read BOP ``scene_camera_<cam>.json`` files (camera_utils.py:6-20).
+
+    Returns ``{cam: {'K': {im_id: f32[3,3]}, 'R': {im_id: f32[3,3]}, 't': {im_id: f32[3]}}}``.
+    """
+    params: Dict[str, Dict[str, dict]] = {}
+    for cam in cam_ids:
+        path = os.path.join(scene_dir, f"scene_camera_{cam}.json")
+        with open(path) as fh:
+            records = json.load(fh)
+        per_cam = {"K": {}, "R": {}, "t": {}}
+        for key, rec in records.items():
+            im_id = int(key)
+            per_cam["K"][im_id] = np.asarray(rec["cam_K"], dtype=np.float32).reshape(3, 3)
+            per_cam["R"][im_id] = np.asarray(rec["cam_R_w2c"], dtype=np.float32).reshape(3, 3)
+            per_cam["t"][im_id] = np.asarray(rec["cam_t_w2c"], dtype=np.float32).reshape(-1)
+        params[cam] = per_cam
+    return params
+
+
+def calc_pose_matrix(R_mat: np.ndarray, t: np.ndarray) -> np.ndarray:
+    """4x4 float64 [R|t] (data_utils.py:383-387: built on ``np.eye(4)``)."""
+    pose = np.eye(4)
+    pose[:3, :3] = R_mat
+    pose[:3, 3] = t
+    return pose
+
+
+def compute_fundamental_matrix(K1, R1, t1, K2, R2, t2) -> np.ndarray:
+    """F mapping camera-1 points to camera-2 epipolar lines (camera_utils.py:23-46).
+
+    ``F = K2^-T [t_rel]_x R_rel K1^-1`` with ``R_rel = R2 R1^T``,
+    ``t_rel = t2 - R_rel t1``; normalised by F[2,2] when |F[2,2]| > 1e-8.
+    """
+    t1 = np.asarray(t1).reshape(-1)
+    t2 = np.asarray(t2).reshape(-1)
+    R_rel = R2 @ R1.T
+    t_rel = t2 - R_rel @ t1
+    # the reference builds the skew matrix as float32 (camera_utils.py:31-35)
+    skew = np.zeros((3, 3), dtype=np.float32)
+    skew[0, 1], skew[0, 2] = -t_rel[2], t_rel[1]
+    skew[1, 0], skew[1, 2] = t_rel[2], -t_rel[0]
+    skew[2, 0], skew[2, 1] = -t_rel[1], t_rel[0]
+    essential = skew @ R_rel
+    F = np.linalg.inv(K2).T @ essential @ np.linalg.inv(K1)
+    if abs(F[2, 2]) > 1e-8:
+        F /= F[2, 2]
+    return F
+
+
+def camera_pairs(n_cams: int) -> np.ndarray:
+    """All camera pairs (a, b), a < b, in lexicographic order -> int32 [P, 2].
+
+    For three cameras this is (0,1), (0,2), (1,2): the F12, F13, F23 of
+    ``process_pose.py:157-159``.
+    """
+    out = [(a, b) for a in range(n_cams) for b in range(a + 1, n_cams)]
+    return np.asarray(out, dtype=np.int32).reshape(-1, 2)
+
+
+def fundamental_matrices(Ks: Sequence[np.ndarray], RTs: Sequence[np.ndarray],
+                         pairs: np.ndarray) -> np.ndarray:
+    """F for every listed pair of one capture -> float64 [P, 9] (row-major)."""
+    out = np.empty((len(pairs), 9), dtype=np.float64)
+    for p, (a, b) in enumerate(pairs):
+        F = compute_fundamental_matrix(Ks[a], RTs[a][:3, :3], RTs[a][:3, 3],
+                                       Ks[b], RTs[b][:3, :3], RTs[b][:3, 3])
+        out[p] = np.asarray(F, dtype=np.float64).reshape(9)
+    return out

@@ -1,0 +1,248 @@
+"""PyTorch custom ops over the C ABI (``torch.ops.mvmatch.*``).
+
+Each op is a thin shim: it validates dtypes/devices/shapes, then calls the
+corresponding ``include/mvmatch.h`` entry point on the tensors' device
+pointers and the current HIP stream.  Nothing here computes on the host.
+
+Ops (all ``*_out`` ops write caller-allocated tensors, like the C ABI):
+  mvmatch::pairwise_residual_argmin_out   e_ab (f32) + per-row argmin/min
+  mvmatch::pairwise_residual_f64_out      e_ab kept in float64 (uniform layout)
+  mvmatch::triplet_cost_argmin_out        3-camera cube + per-(i,j) argmin
+
+Plans (``PairwisePlan`` / ``TripletPlan``) hold the host-side offset tables
+(prefix sums of the per-view detection counts) and their device copies; a
+plan is reusable for every batch with the same counts.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import numpy as np
+import torch
+from torch import Tensor
+
+from . import _native
+
+__all__ = [
+    "PairwisePlan", "TripletPlan",
+    "pairwise_residual_argmin", "pairwise_residual_f64", "triplet_cost_argmin",
+]
+
+
+def _p(t: Optional[Tensor]):
+    if t is None or t.numel() == 0:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(t: Tensor):
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _require(t: Tensor, name: str, dtype: torch.dtype, device: torch.device) -> None:
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: expected device {device}, got {t.device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+
+
+def _check_inputs(pts: Tensor, cam_offs: Tensor, F: Tensor, n_views: int, n_mats: int) -> None:
+    if pts.device.type != "cuda":
+        raise ValueError("pts must be a GPU tensor (the matcher has no CPU path)")
+    dev = pts.device
+    _require(pts, "pts", torch.float64, dev)
+    _require(cam_offs, "cam_offs", torch.int64, dev)
+    _require(F, "F", torch.float64, dev)
+    if pts.dim() != 2 or pts.shape[1] != 2:
+        raise ValueError(f"pts: expected [n, 2], got {tuple(pts.shape)}")
+    if cam_offs.numel() != n_views + 1:
+        raise ValueError(f"cam_offs: expected {n_views + 1} entries, got {cam_offs.numel()}")
+    if F.numel() != n_mats * 9:
+        raise ValueError(f"F: expected {n_mats} 3x3 matrices, got {F.numel()} values")
+
+
+# ------------------------------------------------------------------ ops ----
+@torch.library.custom_op("mvmatch::pairwise_residual_argmin_out",
+                         mutates_args=("dist", "argmin", "minval"))
+def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: List[int],
+                                 pair_b: List[int], n_scenes: int, n_cams: int, max_rows: int,
+                                 dist_offs: Tensor, row_offs: Tensor, dist: Tensor,
+                                 argmin: Tensor, minval: Tensor) -> None:
+    n_pairs = len(pair_a)
+    _check_inputs(pts, cam_offs, F, n_scenes * n_cams, n_scenes * n_pairs)
+    for t, n, dt in ((dist_offs, "dist_offs", torch.int64), (row_offs, "row_offs", torch.int64),
+                     (dist, "dist", torch.float32), (argmin, "argmin", torch.int32),
+                     (minval, "minval", torch.float32)):
+        _require(t, n, dt, pts.device)
+    pa = (ctypes.c_int32 * n_pairs)(*pair_a)
+    pb = (ctypes.c_int32 * n_pairs)(*pair_b)
+    st = _native.load().mvm_pairwise_residual_argmin(
+        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_rows,
+        _p(dist_offs), _p(row_offs), _p(dist), _p(argmin), _p(minval), _stream(pts))
+    _native.check("mvm_pairwise_residual_argmin", st)
+
+
+@pairwise_residual_argmin_out.register_fake
+def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_rows, dist_offs, row_offs, dist,
+      argmin, minval):
+    return None
+
+
+@torch.library.custom_op("mvmatch::pairwise_residual_f64_out", mutates_args=("e",))
+def pairwise_residual_f64_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: List[int],
+                              pair_b: List[int], n_scenes: int, n_cams: int, max_rows: int,
+                              mat_stride: int, ld: int, e: Tensor) -> None:
+    n_pairs = len(pair_a)
+    _check_inputs(pts, cam_offs, F, n_scenes * n_cams, n_scenes * n_pairs)
+    _require(e, "e", torch.float64, pts.device)
+    if e.numel() < n_scenes * n_pairs * mat_stride:
+        raise ValueError("e: too small for n_scenes * n_pairs * mat_stride")
+    pa = (ctypes.c_int32 * n_pairs)(*pair_a)
+    pb = (ctypes.c_int32 * n_pairs)(*pair_b)
+    st = _native.load().mvm_pairwise_residual_f64(
+        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_rows, mat_stride,
+        ld, _p(e), _stream(pts))
+    _native.check("mvm_pairwise_residual_f64", st)
+
+
+@pairwise_residual_f64_out.register_fake
+def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_rows, mat_stride, ld, e):
+    return None
+
+
+@torch.library.custom_op("mvmatch::triplet_cost_argmin_out",
+                         mutates_args=("cube", "argmin", "minval", "workspace"))
+def triplet_cost_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, max_n: int,
+                            cube_offs: Tensor, row_offs: Tensor, cube: Tensor, argmin: Tensor,
+                            minval: Tensor, workspace: Tensor) -> None:
+    _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
+    for t, n, dt in ((cube_offs, "cube_offs", torch.int64), (row_offs, "row_offs", torch.int64),
+                     (cube, "cube", torch.float32), (argmin, "argmin", torch.int32),
+                     (minval, "minval", torch.float32), (workspace, "workspace", torch.uint8)):
+        _require(t, n, dt, pts.device)
+    ws_bytes = workspace.numel()
+    st = _native.load().mvm_triplet_cost_argmin(
+        _p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(cube_offs), _p(row_offs), _p(cube),
+        _p(argmin), _p(minval), _p(workspace), ws_bytes, _stream(pts))
+    _native.check("mvm_triplet_cost_argmin", st)
+
+
+@triplet_cost_argmin_out.register_fake
+def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minval, workspace):
+    return None
+
+
+# ---------------------------------------------------------------- plans ----
+class PairwisePlan:
+    """Offsets of every (scene, pair) residual matrix and argmin row block.
+
+    Built on the host from ``cam_offs`` (the per-view counts are host
+    knowledge: they come from the detector), copied once to ``device``.
+    """
+
+    def __init__(self, cam_offs: np.ndarray, n_scenes: int, n_cams: int, pairs,
+                 device: torch.device | str = "cuda"):
+        cam_offs = np.asarray(cam_offs, dtype=np.int64)
+        pairs = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
+        counts = np.diff(cam_offs).reshape(n_scenes, n_cams)
+        na = counts[:, pairs[:, 0]].reshape(-1)
+        nb = counts[:, pairs[:, 1]].reshape(-1)
+        dist_offs = np.zeros(na.size + 1, np.int64)
+        row_offs = np.zeros(na.size + 1, np.int64)
+        np.cumsum(na * nb, out=dist_offs[1:])
+        np.cumsum(na, out=row_offs[1:])
+        self.n_scenes, self.n_cams = int(n_scenes), int(n_cams)
+        self.pairs = pairs
+        self.pair_a = [int(a) for a in pairs[:, 0]]
+        self.pair_b = [int(b) for b in pairs[:, 1]]
+        self.max_rows = int(na.max()) if na.size else 0
+        self.max_cols = int(nb.max()) if nb.size else 0
+        self.na, self.nb = na, nb
+        self.n_dist = int(dist_offs[-1])
+        self.n_rows = int(row_offs[-1])
+        self.dist_offs_host, self.row_offs_host = dist_offs, row_offs
+        self.device = torch.device(device)
+        self.dist_offs = torch.from_numpy(dist_offs).to(self.device)
+        self.row_offs = torch.from_numpy(row_offs).to(self.device)
+
+    def matrix(self, dist: Tensor, scene: int, pair: int) -> Tensor:
+        """View of the (scene, pair) residual matrix inside a flat ``dist``."""
+        sp = scene * len(self.pair_a) + pair
+        o = int(self.dist_offs_host[sp])
+        na, nb = int(self.na[sp]), int(self.nb[sp])
+        return dist[o:o + na * nb].view(na, nb)
+
+
+def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: PairwisePlan, *,
+                             want_dist: bool = True,
+                             out: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
+    """-> (dist f32 [plan.n_dist], argmin i32 [plan.n_rows], minval f32 [plan.n_rows])."""
+    dev = pts.device
+    if out is None:
+        dist = torch.empty(plan.n_dist if want_dist else 0, dtype=torch.float32, device=dev)
+        argmin = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
+        minval = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
+    else:
+        dist, argmin, minval = out
+    torch.ops.mvmatch.pairwise_residual_argmin_out(
+        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_rows,
+        plan.dist_offs, plan.row_offs, dist, argmin, minval)
+    return dist, argmin, minval
+
+
+def pairwise_residual_f64(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: PairwisePlan):
+    """fp64 residual matrices -> Tensor [S*P, max_rows, ld] (padding unspecified)."""
+    ld = (max(plan.max_cols, 1) + 3) // 4 * 4
+    rows = max(plan.max_rows, 1)
+    e = torch.zeros(plan.n_scenes * len(plan.pair_a) * rows * ld, dtype=torch.float64,
+                    device=pts.device)
+    torch.ops.mvmatch.pairwise_residual_f64_out(
+        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_rows,
+        rows * ld, ld, e)
+    return e.view(plan.n_scenes * len(plan.pair_a), rows, ld)
+
+
+class TripletPlan:
+    """Offsets + workspace for batched 3-camera cubes (cam_offs has S*3+1 entries)."""
+
+    def __init__(self, cam_offs: np.ndarray, n_scenes: int, device: torch.device | str = "cuda"):
+        cam_offs = np.asarray(cam_offs, dtype=np.int64)
+        counts = np.diff(cam_offs).reshape(n_scenes, 3)
+        rows = counts[:, 0] * counts[:, 1]
+        cube_offs = np.zeros(n_scenes + 1, np.int64)
+        row_offs = np.zeros(n_scenes + 1, np.int64)
+        np.cumsum(rows * counts[:, 2], out=cube_offs[1:])
+        np.cumsum(rows, out=row_offs[1:])
+        self.n_scenes = int(n_scenes)
+        self.counts = counts
+        self.max_n = int(counts.max()) if counts.size else 0
+        self.n_cube = int(cube_offs[-1])
+        self.n_rows = int(row_offs[-1])
+        self.cube_offs_host, self.row_offs_host = cube_offs, row_offs
+        self.device = torch.device(device)
+        self.cube_offs = torch.from_numpy(cube_offs).to(self.device)
+        self.row_offs = torch.from_numpy(row_offs).to(self.device)
+        self.workspace_bytes = int(_native.load().mvm_triplet_workspace_bytes(self.n_scenes,
+                                                                               self.max_n))
+        self.workspace = torch.empty(max(self.workspace_bytes, 16), dtype=torch.uint8,
+                                     device=self.device)
+
+
+def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
+                        want_cube: bool = True,
+                        out: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
+    """-> (cube f32 [plan.n_cube], argmin i32 [plan.n_rows], minval f32 [plan.n_rows])."""
+    dev = pts.device
+    if out is None:
+        cube = torch.empty(plan.n_cube if want_cube else 0, dtype=torch.float32, device=dev)
+        argmin = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
+        minval = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
+    else:
+        cube, argmin, minval = out
+    torch.ops.mvmatch.triplet_cost_argmin_out(
+        pts, cam_offs, F, plan.n_scenes, plan.max_n, plan.cube_offs, plan.row_offs, cube, argmin,
+        minval, plan.workspace)
+    return cube, argmin, minval

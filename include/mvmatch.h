@@ -1,0 +1,121 @@
+/*
+ * mvmatch.h — C ABI of the MI355X multi-view epipolar matcher.
+ *
+ * This is the drop-in boundary for the hot path of the reference's
+ * bpc/inference/epipolar_matching.py.  The reference's boundary is a Python
+ * function-call boundary (process_pose.py:24 binds compute_cost_matrix /
+ * match_objects by name; camera_utils.compute_fundamental_matrix is bound at
+ * process_pose.py:26); the entry points below are what that module's compute
+ * reduces to once the O(n^2)/O(n^3) loops move to the GPU.  Python binds them
+ * with ctypes (bpc_baseline_amd/_native.py) and registers them as PyTorch
+ * custom ops (bpc_baseline_amd/ops.py); INTEGRATION.md shows the bindings.
+ *
+ * Conventions
+ *   - every pointer argument named *_dev is a caller-allocated DEVICE pointer;
+ *     pointers without the suffix are host pointers;
+ *   - work is enqueued on `stream` (a hipStream_t; NULL = default stream) and
+ *     nothing is synchronised: results are ready when the stream reaches them;
+ *   - no allocation, no host<->device copy and no global mutable state in any
+ *     launch function (safe to capture in a hipGraph, re-entrant per stream);
+ *   - return value: MVM_OK or an MVM_ERR_* code; mvm_last_error_string()
+ *     gives a per-thread message for the last failing call.
+ *
+ * Detections use a CSR layout: pts_dev holds (x, y) float64 centroids of all
+ * detections, scene-major then camera-minor; cam_offs_dev[s*C + c] ..
+ * cam_offs_dev[s*C + c + 1] is the detection range of camera c in scene s.
+ * Fundamental matrices are float64, row-major, one per (scene, pair):
+ * F_dev[(s*P + p)*9 + 3*r + c] = F[r][c] with F mapping camera pair_a[p]
+ * points to camera pair_b[p] epipolar lines (camera_utils.py:23-46).
+ */
+#ifndef MVMATCH_H
+#define MVMATCH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVM_ABI_VERSION 1
+#define MVM_MAX_CAMS 8
+#define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
+
+typedef struct ihipStream_t *mvm_stream_t; /* == hipStream_t */
+
+enum {
+    MVM_OK = 0,
+    MVM_ERR_INVALID_ARGUMENT = 1, /* null pointer, negative size, bad pair index */
+    MVM_ERR_UNSUPPORTED = 2,      /* more cameras/pairs than MVM_MAX_* */
+    MVM_ERR_WORKSPACE = 3,        /* workspace smaller than required */
+    MVM_ERR_HIP = 4               /* a HIP runtime call or kernel launch failed */
+};
+
+/* Library version string ("mvmatch <semver> gfx950"). */
+const char *mvm_version(void);
+/* Message of the last failing call on this thread ("" if none). */
+const char *mvm_last_error_string(void);
+/* Static description of a status code. */
+const char *mvm_status_string(int status);
+
+/*
+ * Pairwise symmetric epipolar residuals + per-row argmin, batched over
+ * (scene, camera pair).  Replaces the per-pair epipolar_error calls
+ * (bpc/inference/epipolar_matching.py:5-28) with one launch; the per-row
+ * argmin is SURVEY §8a row a5 (oracle: np.argmin(e_ab, axis=1)).
+ *
+ * For scene s and pair p = (a, b), with n_a, n_b detections in cameras a, b:
+ *   e[i][j] = float32(epipolar_error(p_a[i], p_b[j], F[s, p]))       (fp64 math)
+ *   dist_dev[dist_offs_dev[s*P + p] + i*n_b + j] = e[i][j]
+ *   argmin_dev[row_offs_dev[s*P + p] + i] = lowest j minimising e[i][:]
+ *                                             (NaN counts as smallest; -1 if n_b == 0)
+ *   minval_dev[...]                         = e[i][argmin] (NaN if n_b == 0)
+ * dist_dev, argmin_dev and minval_dev may each be NULL (not produced).
+ * pair_a / pair_b are HOST arrays of n_pairs camera indices (a != b).
+ * max_rows is a host-known upper bound on n_a over all (scene, pair): it only
+ * sizes the grid (rows beyond the real n_a are skipped on the device).
+ */
+int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
+                                 const double *F_dev, const int32_t *pair_a,
+                                 const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                 int32_t n_pairs, int32_t max_rows, const int64_t *dist_offs_dev,
+                                 const int64_t *row_offs_dev, float *dist_dev,
+                                 int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream);
+
+/*
+ * Same residuals kept in float64 (no cast), written with a uniform layout:
+ * matrix (s, p) starts at e_dev + (s*P + p) * mat_stride and has row stride
+ * ld (>= every n_b; use a multiple of 4 for vectorised stores).  This is the
+ * exact fp64 value of epipolar_error (epipolar_matching.py:28) and the input
+ * of the three-camera cube.
+ */
+int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev,
+                              const double *F_dev, const int32_t *pair_a, const int32_t *pair_b,
+                              int32_t n_scenes, int32_t n_cams, int32_t n_pairs,
+                              int32_t max_rows, int64_t mat_stride, int64_t ld, double *e_dev,
+                              mvm_stream_t stream);
+
+/*
+ * Three-camera cost cube + per-(i,j) argmin over k, batched over scenes.
+ * Replaces compute_cost_matrix (epipolar_matching.py:83-98):
+ *   cube[i][j][k] = float32(((e12[i][j] + e13[i][k]) + e23[j][k]) / 3)
+ * with e_ab the fp64 residuals of pairs (0,1), (0,2), (1,2); F_dev holds
+ * F12, F13, F23 for every scene ([S*3, 9]); cam_offs_dev has S*3+1 entries.
+ *   cube_dev[cube_offs_dev[s] + (i*M + j)*P + k]
+ *   argmin_dev[row_offs_dev[s] + i*M + j]   (argmin over k of the flattened
+ *                                            (N*M, P) cube row; -1 if P == 0)
+ * max_n bounds every view's detection count.  workspace_dev must hold
+ * mvm_triplet_workspace_bytes(n_scenes, max_n) bytes (16-byte aligned).
+ */
+size_t mvm_triplet_workspace_bytes(int32_t n_scenes, int32_t max_n);
+int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
+                            const double *F_dev, int32_t n_scenes, int32_t max_n,
+                            const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                            float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                            void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MVMATCH_H */

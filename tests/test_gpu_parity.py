@@ -1,0 +1,179 @@
+"""GPU parity: HIP kernels (through the C ABI / torch ops) vs the pinned oracle
+and the reference's golden vectors.  Bit-exact is the bar: float32 outputs are
+compared as bit patterns, argmin indices exactly."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.int32)
+
+
+def run_pairwise(dev, pts, cam_offs, F, pairs, S, C, want_dist=True):
+    from bpc_baseline_amd import ops
+    plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=dev)
+    d, a, m = ops.pairwise_residual_argmin(
+        torch.from_numpy(np.ascontiguousarray(pts, np.float64)).to(dev),
+        torch.from_numpy(np.ascontiguousarray(cam_offs, np.int64)).to(dev),
+        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan, want_dist=want_dist)
+    torch.cuda.synchronize()
+    return d.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
+
+
+def run_cube(dev, pts, cam_offs, F, S):
+    from bpc_baseline_amd import ops
+    plan = ops.TripletPlan(cam_offs, S, device=dev)
+    c, a, m = ops.triplet_cost_argmin(
+        torch.from_numpy(np.ascontiguousarray(pts, np.float64)).to(dev),
+        torch.from_numpy(np.ascontiguousarray(cam_offs, np.int64)).to(dev),
+        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan)
+    torch.cuda.synchronize()
+    return c.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
+
+
+def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
+    d, a, m = run_pairwise(dev, pts, cam_offs, F, pairs, S, C)
+    rd, ra, rm, _, _ = O.pairwise(pts, cam_offs, F, pairs, S, C)
+    assert d.shape == rd.shape
+    bad = np.nonzero(_bits(d) != _bits(rd))[0]
+    assert bad.size == 0, f"{bad.size} dist mismatches, first at {bad[:5]}: {d[bad[:5]]} vs {rd[bad[:5]]}"
+    assert np.array_equal(a, ra), f"argmin mismatches at {np.nonzero(a != ra)[0][:10]}"
+    assert np.array_equal(_bits(m), _bits(rm))
+
+
+# ----------------------------------------------------------- pairwise ----
+@pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),
+                                          (4, 3, 37, True), (2, 2, 1, False), (3, 6, 130, True)])
+def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged):
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(S, C, n, seed=100 + S * n, ragged=ragged)
+    assert_pairwise_equal(cuda, b.pts, b.cam_offs, b.F, b.pairs, S, C)
+
+
+def test_pairwise_golden_4cam(cuda, golden):
+    """Reference epipolar_error over every pair of a 4-camera capture (empty view, duplicates)."""
+    g = golden("a5_pairwise.npz")
+    pairs = g["pairs"]
+    views = [g[f"pts{c}"] for c in range(4)]
+    cam_offs = np.zeros(5, np.int64)
+    np.cumsum([len(v) for v in views], out=cam_offs[1:])
+    pts = np.concatenate(views)
+    d, a, _ = run_pairwise(cuda, pts, cam_offs, g["F"], pairs, 1, 4)
+    from bpc_baseline_amd.ops import PairwisePlan
+    plan = PairwisePlan(cam_offs, 1, 4, pairs, device="cpu")
+    for p, (ca, cb) in enumerate(pairs):
+        ref = g[f"e{ca}{cb}"]
+        got = plan.matrix(torch.from_numpy(d), 0, p).numpy()
+        assert got.shape == ref.shape
+        assert np.array_equal(_bits(got), _bits(ref)), f"pair {ca}{cb}"
+        ro = plan.row_offs_host
+        assert np.array_equal(a[ro[p]:ro[p + 1]], g[f"argmin{ca}{cb}"])
+
+
+def test_pairwise_f64_kats(cuda, golden):
+    """Every scalar epipolar_error KAT as its own scene: fp64 bits must match the reference."""
+    from bpc_baseline_amd import ops
+    g = golden("a1_epipolar_error.npz")
+    n = len(g["e"])
+    pts = np.stack([g["p1"], g["p2"]], axis=1).reshape(-1, 2)
+    cam_offs = np.arange(2 * n + 1, dtype=np.int64)
+    plan = ops.PairwisePlan(cam_offs, n, 2, [[0, 1]], device=cuda)
+    e = ops.pairwise_residual_f64(torch.from_numpy(pts).to(cuda), torch.from_numpy(cam_offs).to(cuda),
+                                  torch.from_numpy(g["F"].copy()).to(cuda), plan)
+    got = e[:, 0, 0].cpu().numpy()
+    bad = np.nonzero(got.view(np.int64) != g["e"].view(np.int64))[0]
+    assert bad.size == 0, f"{bad.size} fp64 mismatches (kinds {np.unique(g['kind'][bad])}): " \
+                          f"{got[bad[:3]]} vs {g['e'][bad[:3]]}"
+
+
+def test_pairwise_edge_cases(cuda):
+    """Degenerate lines (9999 sentinel), NaN / inf / huge centroids, tails, misalignment."""
+    rng = np.random.default_rng(5)
+    C, S = 3, 6
+    counts = np.array([[5, 7, 3], [1, 1, 1], [9, 0, 4], [3, 6, 5], [2, 3, 2], [6, 5, 7]])
+    cam_offs = np.zeros(S * C + 1, np.int64)
+    np.cumsum(counts.reshape(-1), out=cam_offs[1:])
+    pts = np.floor(rng.uniform(0, 4800, size=(cam_offs[-1], 2))) / 2
+    pts[3] = [np.nan, 4.0]
+    pts[9] = [np.inf, 1.0]
+    pts[20] = [1e300, -1e300]
+    pts[21] = [2.0 ** 41, 7.0]
+    pairs = np.array([[0, 1], [0, 2], [1, 2]], np.int32)
+    F = rng.normal(size=(S * 3, 9))
+    F[0, 0:6] = 0.0             # degenerate row lines (F rows 0,1 = 0)
+    F[1, [0, 1, 3, 4, 6, 7]] = 0.0   # degenerate column lines (F cols 0,1 = 0)
+    F[2] = 0.0                  # both
+    F[5] *= 1e-9                # norms near the 1e-8 threshold
+    F[7, 2] = 1e70              # huge l2
+    assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C)
+
+
+def test_pairwise_ties_and_duplicates(cuda):
+    """Duplicate detections give exact ties across lanes and chunks: lowest index wins."""
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(2, 3, 600, seed=3)
+    pts = b.pts.copy()
+    # cam 1 of scene 0: copy column 3 into columns 300 and 517 (other chunk / other lane)
+    o = b.cam_offs[1]
+    pts[o + 300] = pts[o + 3]
+    pts[o + 517] = pts[o + 3]
+    pts[o + 4] = pts[o + 3]
+    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3)
+
+
+def test_pairwise_argmin_only(cuda):
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(2, 4, 200, seed=9)
+    d, a, m = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False)
+    _, ra, rm, _, _ = O.pairwise(b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False)
+    assert d.size == 0
+    assert np.array_equal(a, ra) and np.array_equal(_bits(m), _bits(rm))
+
+
+# --------------------------------------------------------------- cube ----
+def test_cube_golden_batched(cuda, golden):
+    """All reference compute_cost_matrix cubes in ONE ragged batched launch."""
+    g = golden("a3_cost_cubes.npz")
+    names = list(g["names"])
+    views, Fs = [], []
+    for n in names:
+        views += [g[f"{n}_p1"], g[f"{n}_p2"], g[f"{n}_p3"]]
+        Fs.append(g[f"{n}_F"])
+    cam_offs = np.zeros(len(views) + 1, np.int64)
+    np.cumsum([len(v) for v in views], out=cam_offs[1:])
+    c, a, _ = run_cube(cuda, np.concatenate(views), cam_offs, np.concatenate(Fs), len(names))
+    co = ro = 0
+    for n in names:
+        ref = g[f"{n}_cube"]
+        N, M, P = ref.shape
+        got = c[co:co + ref.size]
+        assert np.array_equal(_bits(got), _bits(ref.reshape(-1))), f"cube {n}"
+        assert np.array_equal(a[ro:ro + N * M], g[f"{n}_argmin"]), f"argmin {n}"
+        co += ref.size
+        ro += N * M
+
+
+@pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False)])
+def test_cube_synthetic_vs_oracle(cuda, S, n, ragged):
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
+    c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S)
+    rc, ra, rm, _, _ = O.cube(b.pts, b.cam_offs, b.F, S)
+    bad = np.nonzero(_bits(c) != _bits(rc))[0]
+    assert bad.size == 0, f"{bad.size} cube mismatches"
+    assert np.array_equal(a, ra)
+    assert np.array_equal(_bits(m), _bits(rm))
+
+
+def test_deterministic_repeat(cuda):
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(4, 4, 700, seed=1)
+    r1 = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 4, 4)
+    r2 = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 4, 4)
+    for x, y in zip(r1, r2):
+        assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
