@@ -1,0 +1,348 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X multi-view epipolar matcher (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c2cube]
+
+A *step* is one pass of the hot path over this rank's whole batch of
+synthetic scenes (resident in HBM): pairwise symmetric epipolar residuals for
+every (scene, camera pair, detection_i, detection_j), written as float32
+matrices, plus the per-row argmin association; for N > 1 the step ends with
+the single gather of every rank's association rows to rank 0 (RCCL/xGMI).
+
+Default workload (``c3``, BASELINE.json configs[2], the configuration the
+@1/2/4/8-GPU metric is quoted on via configs[3]): 4 cameras x 1024
+detections/view x 10,000 scenes PER GPU (weak scaling: each rank owns its own
+10k-scene shard), 6 camera pairs -> 6.29e10 detection pairs per GPU per step.
+Scenes are processed in launches of ``--chunk`` scenes; every residual is
+stored to HBM (a chunk-sized buffer is reused across launches).
+
+Printed by rank 0: ONE JSON line with value = total pairs/s over all ranks,
+the dominant kernel's roofline (achieved algorithmic GB/s from HIP events on
+the launch stream vs the 8 TB/s HBM peak) and a CPU baseline (the C/OpenMP
+restatement in oracle/, timed on a bounded sample on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+from bpc_baseline_amd import ops  # noqa: E402
+from bpc_baseline_amd.distributed import gather_rows, init_from_env, max_over_ranks  # noqa: E402
+from bpc_baseline_amd.synth import make_scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "detection-pairs matched/sec"
+
+WORKLOADS = {
+    "c3": dict(n_cams=4, n_dets=1024, n_scenes=10000, chunk=1000, mode="pairwise",
+               desc="C3: synthetic IPD-like 4-cam x 1024 dets/view x 10000 scenes per GPU, "
+                    "pairwise residual matrices + per-row argmin"),
+    "c2": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=1000, mode="pairwise",
+               desc="C2: synthetic IPD-like 3-cam x 256 dets/view x 1000 scenes per GPU, "
+                    "pairwise residual matrices + per-row argmin"),
+    "c2cube": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=250, mode="cube",
+                   desc="C2 cube: 3-cam x 256 dets/view x 1000 scenes per GPU, "
+                        "compute_cost_matrix cubes + per-(i,j) argmin (units = triples)"),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pairwise_bytes(counts: np.ndarray, pairs: np.ndarray) -> float:
+    """Algorithmic HBM bytes of one pairwise launch:
+    16 B per centroid read + 72 B per F + per pair matrix 4 B/pair + 8 B/row."""
+    na = counts[:, pairs[:, 0]].astype(np.float64)
+    nb = counts[:, pairs[:, 1]].astype(np.float64)
+    return float(16.0 * counts.sum() + 72.0 * na.size + (4.0 * na * nb + 8.0 * na).sum())
+
+
+def cube_bytes(counts: np.ndarray) -> float:
+    """Cube launch: centroids + 3 F + 4 B/triple + 8 B per (i,j) row."""
+    N, M, P = (counts[:, k].astype(np.float64) for k in range(3))
+    return float(16.0 * counts.sum() + 3 * 72.0 * len(N) + (4.0 * N * M * P + 8.0 * N * M).sum())
+
+
+class Chunk:
+    def __init__(self, s0, pts, cam_offs, F, plan, row_base, units, nbytes):
+        self.s0 = s0
+        self.pts, self.cam_offs, self.F, self.plan = pts, cam_offs, F, plan
+        self.row_base, self.units, self.nbytes = row_base, units, nbytes
+
+
+def build_chunks(batch, chunk, device, mode):
+    C, P = batch.n_cams, batch.n_pairs
+    pts_all = torch.from_numpy(batch.pts).to(device)
+    F_all = torch.from_numpy(batch.F).to(device)
+    counts = batch.counts()
+    chunks, row_base = [], 0
+    for s0 in range(0, batch.n_scenes, chunk):
+        s1 = min(batch.n_scenes, s0 + chunk)
+        co = batch.cam_offs[s0 * C:s1 * C + 1]
+        base = int(co[0])
+        co_rel = (co - base).astype(np.int64)
+        pts = pts_all[base:int(co[-1])]
+        F = F_all[s0 * P:s1 * P]
+        if mode == "pairwise":
+            plan = ops.PairwisePlan(co_rel, s1 - s0, C, batch.pairs, device=device)
+            units = int(plan.n_dist)
+            nbytes = pairwise_bytes(counts[s0:s1], batch.pairs)
+        else:
+            plan = ops.TripletPlan(co_rel, s1 - s0, device=device)
+            units = int(plan.n_cube)
+            nbytes = cube_bytes(counts[s0:s1])
+        chunks.append(Chunk(s0, pts, torch.from_numpy(co_rel).to(device), F, plan, row_base, units,
+                            nbytes))
+        row_base += plan.n_rows
+    return chunks, row_base
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, int(n))
+
+
+def cpu_baseline(batch, mode: str, target_s: float):
+    """Time the C/OpenMP restatement (oracle/, test infrastructure) on a bounded
+    sample of this workload's scenes -> dict for the JSON line."""
+    from oracle import oracle as O
+    threads = cpu_threads()
+    C = batch.n_cams
+
+    def run(n_sc):
+        co = batch.cam_offs[:n_sc * C + 1]
+        pts = batch.pts[:int(co[-1])]
+        t0 = time.perf_counter()
+        if mode == "pairwise":
+            d, _, _, _, _ = O.pairwise(pts, co, batch.F[:n_sc * batch.n_pairs], batch.pairs, n_sc, C,
+                                       nthreads=threads)
+            units = d.size
+        else:
+            c, _, _, _, _ = O.cube(pts, co, batch.F[:n_sc * 3], n_sc, nthreads=threads)
+            units = c.size
+        return units, time.perf_counter() - t0
+
+    run(1)                                           # warm (page-in, thread pool)
+    u1, t1 = run(min(batch.n_scenes, max(1, threads)))
+    per_scene = t1 / min(batch.n_scenes, max(1, threads))
+    n_sc = int(min(batch.n_scenes, max(1, round(target_s / max(per_scene, 1e-9)))))
+    units, secs = run(n_sc)
+    unit = "pairs/s" if mode == "pairwise" else "triples/s"
+    return {"value": units / secs, "unit": unit, "cores": threads, "kind": "port",
+            "sample": f"{n_sc} scenes ({units:.3g} {unit[:-2]}) of this workload in {secs:.1f} s, "
+                      f"oracle/mvm_oracle.c fp64 restatement (bit-exact to the reference), "
+                      f"OpenMP x{threads} on {cpu_model()}"}
+
+
+def load_traffic(workload: str):
+    path = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            rec = json.load(fh).get(workload)
+        return rec
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (override)")
+    ap.add_argument("--chunk", type=int, default=None, help="scenes per launch (override)")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
+                    help="weak: --scenes per GPU; strong: --scenes split over the GPUs")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target length of the CPU-baseline sample (0 disables)")
+    ap.add_argument("--seed", type=int, default=0)
+    args = ap.parse_args()
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.scenes:
+        wl["n_scenes"] = args.scenes
+    if args.chunk:
+        wl["chunk"] = args.chunk
+
+    env = init_from_env()
+    world = env.world
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+    dev = env.device
+
+    # ---- this rank's shard of scenes (global scene ids are seeds) ----------
+    if args.scaling == "weak":
+        first, n_local = env.rank * wl["n_scenes"], wl["n_scenes"]
+    else:
+        from bpc_baseline_amd.distributed import shard_range
+        a, b = shard_range(wl["n_scenes"], env.rank, world)
+        first, n_local = a, b - a
+    t0 = time.perf_counter()
+    batch = make_scenes(n_local, wl["n_cams"], wl["n_dets"], seed=args.seed, first_scene=first)
+    log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
+    chunks, n_rows = build_chunks(batch, min(wl["chunk"], n_local), dev, wl["mode"])
+    argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
+    minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
+    max_units = max(c.units for c in chunks)
+    dist_buf = torch.empty(max_units, dtype=torch.float32, device=dev)
+    units_local = sum(c.units for c in chunks)
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(c: Chunk):
+        am = argmin[c.row_base:c.row_base + c.plan.n_rows]
+        mv = minval[c.row_base:c.row_base + c.plan.n_rows]
+        if wl["mode"] == "pairwise":
+            ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan,
+                                         out=(dist_buf[:c.units], am, mv))
+        else:
+            ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan,
+                                    out=(dist_buf[:c.units], am, mv))
+
+    def step(events=None):
+        for c in chunks:
+            if events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                launch(c)
+                e1.record(stream)
+                events.append((e0, e1, c))
+            else:
+                launch(c)
+        return gather_rows(env, argmin, minval)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    env.barrier()
+
+    events = []
+    torch.cuda.synchronize(dev)
+    env.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        gathered = step(events)
+    torch.cuda.synchronize(dev)
+    env.barrier()
+    elapsed = time.perf_counter() - t_start
+    elapsed = max_over_ranks(env, elapsed)
+
+    # ---- kernel roofline from the events (on the launch stream) ------------
+    durs = np.array([e0.elapsed_time(e1) * 1e-3 for e0, e1, _ in events])
+    byts = np.array([c.nbytes for _, _, c in events])
+    units_ev = np.array([c.units for _, _, c in events])
+    avg_dur = float(durs.mean())
+    achieved_gbs = float(byts.sum() / durs.sum() / 1e9)
+
+    # ---- parity spot-check of the last launch (untimed) --------------------
+    parity = "skipped"
+    if env.is_root and wl["mode"] == "pairwise":
+        from oracle import oracle as O
+        c = chunks[-1]          # its residuals are still in dist_buf
+        s_first = c.s0
+        C = batch.n_cams
+        co = batch.cam_offs[s_first * C:(s_first + 1) * C + 1]
+        co_rel = co - co[0]
+        rd, ra, _, _, _ = O.pairwise(batch.pts[int(co[0]):int(co[-1])], co_rel,
+                                     batch.F[s_first * batch.n_pairs:(s_first + 1) * batch.n_pairs],
+                                     batch.pairs, 1, C)
+        gd = dist_buf[:rd.size].cpu().numpy()
+        ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
+        ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
+        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rd.size} pairs)"
+    elif env.is_root:
+        parity = "see tests/test_gpu_parity.py"
+
+    # ---- achievable HBM write bandwidth on this box (same store form) -------
+    probe_gbs = None
+    if env.is_root:
+        pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ops.hbm_write_probe(dist_buf)
+        pe0.record(stream)
+        for _ in range(5):
+            ops.hbm_write_probe(dist_buf)
+        pe1.record(stream)
+        torch.cuda.synchronize(dev)
+        probe_gbs = 5 * dist_buf.numel() * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
+
+
+    if not env.is_root:
+        return
+    total_units = units_local * world * args.steps
+    value = total_units / elapsed
+    unit = "pairs/s" if wl["mode"] == "pairwise" else "triples/s"
+    cpu = None
+    if world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(batch, wl["mode"], args.cpu_seconds)
+    traffic = load_traffic(args.workload)
+    out = {
+        "metric": METRIC if wl["mode"] == "pairwise" else "cost-cube triples/sec",
+        "value": value,
+        "unit": unit,
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": args.scaling,
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded IPD-like rig, SURVEY §8d generator)",
+        "config": {
+            "workload": wl["desc"],
+            "n_cams": wl["n_cams"], "n_dets": wl["n_dets"],
+            "n_scenes_per_gpu": n_local if args.scaling == "weak" else None,
+            "n_scenes_total": n_local * world if args.scaling == "weak" else wl["n_scenes"],
+            "scenes_per_launch": wl["chunk"], "launches_per_step": len(chunks),
+            "units_per_gpu_step": units_local,
+            "parallelism": f"scene-sharded x{world}, one RCCL gather per step" if world > 1
+                           else "single GPU",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "pairwise_kernel" if wl["mode"] == "pairwise" else "triplet_kernel",
+            "achieved": achieved_gbs,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "traffic": (traffic or {}).get("bytes_per_launch"),
+            "bytes_per_launch": float(byts.mean()),
+            "avg_launch_ms": avg_dur * 1e3,
+            "units_per_s_in_kernel": float(units_ev.sum() / durs.sum()),
+            "write_probe_gbs": probe_gbs,
+            "frac_of_write_probe": (achieved_gbs / probe_gbs) if probe_gbs else None,
+        },
+        "cpu_baseline": cpu,
+        "parity": parity,
+    }
+    if traffic:
+        out["roofline"]["traffic_source"] = traffic.get("source")
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

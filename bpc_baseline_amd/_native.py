@@ -41,7 +41,7 @@ SIGNATURES = {
     "mvm_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "mvm_pairwise_residual_argmin": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp,            # pts, cam_offs, F, pair_a (host), pair_b (host)
-        _i32, _i32, _i32, _i32,             # n_scenes, n_cams, n_pairs, max_rows
+        _i32, _i32, _i32, _i32,             # n_scenes, n_cams, n_pairs, max_n
         _vp, _vp, _vp, _vp, _vp,            # dist_offs, row_offs, dist, argmin, minval
         _vp]),                              # stream
     "mvm_pairwise_residual_f64": (ctypes.c_int, [
@@ -54,6 +54,7 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
         _vp, _vp, _vp, _vp, _vp,            # cube_offs, row_offs, cube, argmin, minval
         _vp, _sz, _vp]),                    # workspace, workspace_bytes, stream
+    "mvm_hbm_write_probe": (ctypes.c_int, [_vp, _sz, _vp]),
 }
 
 _lib = None

@@ -30,6 +30,7 @@
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "mvmatch.h"
@@ -114,22 +115,43 @@ __device__ __forceinline__ float value_of_key(uint32_t k) {
     return (k == 0u || k == kKeyInvalid) ? __uint_as_float(0x7FC00000u) : __uint_as_float(k - 1u);
 }
 
+// DPP min step: v = min(v, v from the lane DPP control CTRL selects).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
+    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+    return o < v ? o : v;
+}
+
+// Minimum over the wave, returned as a uniform (SGPR) value: four DPP steps
+// reduce each 16-lane row in registers (quad_perm [1,0,3,2], quad_perm
+// [2,3,0,1], row_half_mirror, row_mirror), then the four row minima are read
+// with v_readlane and combined on the scalar unit.  No LDS round trips.
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)v, off, kWave);
-        v = o < v ? o : v;
-    }
-    return v;
+    v = dpp_min<0xB1>(v);
+    v = dpp_min<0x4E>(v);
+    v = dpp_min<0x141>(v);
+    v = dpp_min<0x140>(v);
+    const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+    const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)v, 16);
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)v, 32);
+    const uint32_t d = (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
+    const uint32_t ab = a < b ? a : b, cd = c < d ? c : d;
+    return ab < cd ? ab : cd;
 }
 
 // Reduce (key, idx) over the wave: minimum key, then the lowest column index
-// among the lanes holding it (exact np.argmin tie rule).
+// among the lanes holding it (exact np.argmin tie rule).  A unique minimum
+// (the common case) costs one ballot + one readlane; ties fall back to a
+// second reduction over the candidates' indices.
 __device__ __forceinline__ void wave_argmin(uint32_t key, int32_t idx, uint32_t &kmin,
                                             int32_t &imin) {
     kmin = wave_min_u32(key);
-    const uint32_t cand = (key == kmin) ? (uint32_t)idx : 0x7FFFFFFFu;
-    imin = (int32_t)wave_min_u32(cand);
+    const uint64_t hit = __ballot(key == kmin);
+    if (__builtin_popcountll(hit) == 1) {
+        imin = __builtin_amdgcn_readlane(idx, (int)__builtin_ctzll(hit));
+    } else {
+        imin = (int32_t)wave_min_u32(key == kmin ? (uint32_t)idx : 0x7FFFFFFFu);
+    }
 }
 
 // ----------------------------------------------------------- stores ----
@@ -140,6 +162,16 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void store4_nt(float *dst, const double e[4]) {
     const f32x4 v = {(float)e[0], (float)e[1], (float)e[2], (float)e[3]};
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4 *>(dst));
+}
+typedef f32x4 __attribute__((address_space(1))) g_f32x4;   // global (AS 1) pointee
+
+// Row store from a scalar (SGPR) row address + a 32-bit per-lane byte offset:
+// lowers to `global_store_dwordx4 v_off, v_data, s_base nt` (saddr form, no
+// per-row 64-bit VALU address arithmetic).
+__device__ __forceinline__ void store4_nt_row(uint64_t row_base, uint32_t byte_off,
+                                              const float v4[4]) {
+    const f32x4 v = {v4[0], v4[1], v4[2], v4[3]};
+    __builtin_nontemporal_store(v, reinterpret_cast<g_f32x4 *>(row_base + byte_off));
 }
 __device__ __forceinline__ void store4_nt(double *dst, const double e[4]) {
     const f64x2 lo = {e[0], e[1]}, hi = {e[2], e[3]};
@@ -160,6 +192,8 @@ struct PairArgs {
     int64_t mat_stride;
     int64_t ld;                 // row stride of each matrix; 0 -> n_b
     int32_t n_cams, n_pairs, row_blocks;
+    int32_t rows_per_wg;        // kWaves * RPW * row groups
+    int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -170,52 +204,111 @@ struct ColRegs {
     uint32_t state[kColsPerLane];   // kOk / kDeg / kNone / kWild
 };
 
-// One row of one chunk.  SAFE handles degenerate column lines, non-finite or
-// huge values, chunk tails and unaligned rows; the fast path handles none of
-// them and is chosen only when the whole chunk is clean.
-template <bool SAFE, bool ARGMIN, typename OutT>
-__device__ __forceinline__ void sweep_row(const ColRegs &c, double rl0, double rl1, double rl2,
-                                          double rx, double ry, bool rdeg, OutT *drow,
-                                          int jbase, int nb, uint32_t &bkey, int32_t &bidx) {
+// 0.5 * s for s >= +0 finite, as bits, EXACT after the float32 cast: the
+// saturating decrement of the exponent field halves every s >= 2^-1021
+// exactly, maps +0 to +0, and maps s < 2^-1021 to some fp64 value below
+// 2^-1021 -- which, like the true s/2 < 2^-1022, rounds to float32 +0.
+// One 32-bit op instead of an fp64 multiply.  Used only where the result is
+// consumed as float32 (the f64 output path multiplies by 0.5).
+__device__ __forceinline__ double half_for_f32(double s) {
+    const uint64_t b = (uint64_t)__double_as_longlong(s);
+    const uint32_t hi = __builtin_elementwise_sub_sat((uint32_t)(b >> 32), 0x00100000u);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint32_t)b));
+}
+
+// Running argmin of one row within one lane: best float32 value + its
+// column.  bidx == 0x7FFFFFFF means "no column yet".  Fast-path values are
+// finite, so `v < best` (strict: first occurrence wins) is the whole rule.
+struct Best {
+    float v;
+    int32_t j;
+};
+
+__device__ __forceinline__ void best_update_fast(Best &b, float v, int32_t j) {
+    const bool lt = v < b.v;
+    b.v = lt ? v : b.v;
+    b.j = lt ? j : b.j;
+}
+
+// Generic rule (np.argmin): a NaN beats everything and the first NaN wins;
+// otherwise strict '<'; the first valid column always replaces "none".
+__device__ __forceinline__ void best_update_safe(Best &b, float v, int32_t j) {
+    const bool lt = (b.j == 0x7FFFFFFF) || ((v != v) ? (b.v == b.v) : (v < b.v));
+    b.v = lt ? v : b.v;
+    b.j = lt ? j : b.j;
+}
+
+__device__ __forceinline__ uint32_t best_key(const Best &b) {
+    if (b.j == 0x7FFFFFFF) return kKeyInvalid;
+    return key_of(b.v);
+}
+
+// One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
+// per pair, one 16-byte store, 3 int ops of argmin per pair.
+template <bool ARGMIN, bool STORE, typename OutT>
+__device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
+                                         double rx, double ry, OutT *drow, int jbase, Best &best) {
     double e[kColsPerLane];
+    float v[kColsPerLane];
 #pragma unroll
     for (int q = 0; q < kColsPerLane; ++q) {
-        double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);   // |l1 . p1|
-        if (SAFE) d1 = (c.state[q] == kDeg) ? kSentinel : d1;
-        double d2 = rdeg ? kSentinel : line_dist(rl0, rl1, rl2, c.x[q], c.y[q]);   // |l2 . p2|
-        e[q] = 0.5 * (d1 + d2);                                     // :28
-    }
-    if (drow) {
-        if (!SAFE) {
-            store4_nt(drow + jbase, e);
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];      // l1 . p1
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;         // l2 . p2
+        const double sum = __builtin_fabs(d1) + __builtin_fabs(d2);
+        if constexpr (sizeof(OutT) == 4) {
+            v[q] = (float)half_for_f32(sum);
         } else {
-#pragma unroll
-            for (int q = 0; q < kColsPerLane; ++q)
-                if (jbase + q < nb) __builtin_nontemporal_store((OutT)e[q], drow + jbase + q);
+            e[q] = 0.5 * sum;
         }
     }
-    if (ARGMIN) {
+    if constexpr (sizeof(OutT) == 4) {
+        if (STORE) store4_nt_row(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+        if (ARGMIN) {
 #pragma unroll
-        for (int q = 0; q < kColsPerLane; ++q) {
-            const float v = (float)e[q];
-            uint32_t k = SAFE ? key_of(v) : (__float_as_uint(v) + 1u);
-            if (SAFE && c.state[q] == kNone) k = kKeyInvalid;
-            if (k < bkey) {
-                bkey = k;
-                bidx = jbase + q;
-            }
+            for (int q = 0; q < kColsPerLane; ++q) best_update_fast(best, v[q], jbase + q);
         }
+    } else {
+        if (STORE) store4_nt(drow + jbase, e);
     }
 }
 
+// Generic row: degenerate lines (9999 sentinel), non-finite or huge values,
+// tails, unaligned rows, no output buffer.
+template <bool ARGMIN, typename OutT>
+__device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl1, double rl2,
+                                         double rx, double ry, bool rdeg, OutT *drow, int jbase,
+                                         int nb, Best &best) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);
+        d1 = (c.state[q] == kDeg) ? kSentinel : d1;
+        const double d2 = rdeg ? kSentinel : line_dist(rl0, rl1, rl2, c.x[q], c.y[q]);
+        const double e = 0.5 * (d1 + d2);                                            // :28
+        const bool valid = c.state[q] != kNone;
+        if (drow && valid) __builtin_nontemporal_store((OutT)e, drow + jbase + q);
+        if (ARGMIN && valid) best_update_safe(best, (float)e, jbase + q);
+    }
+}
+
+// Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair).  The
+// normalised lines of (up to col_tile) columns are computed ONCE per
+// workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
+// chunk every lane holds 4 consecutive columns in registers and walks the
+// RPW rows, one coalesced 16-byte store per lane per row.
 template <int RPW, bool ARGMIN, typename OutT>
 __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
-    __shared__ __attribute__((aligned(16))) double s_col[5][kChunk];   // l0 l1 l2 x y
-    __shared__ uint32_t s_cstate[kChunk];
-    __shared__ __attribute__((aligned(16))) double s_row[kWaves * RPW][6];   // l0 l1 l2 x y deg
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int T = args.col_tile;
+    double *s_l0 = reinterpret_cast<double *>(s_dyn);
+    double *s_l1 = s_l0 + T;
+    double *s_l2 = s_l1 + T;
+    double *s_x = s_l2 + T;
+    double *s_y = s_x + T;
+    double(*s_row)[RPW][6] = reinterpret_cast<double(*)[RPW][6]>(s_y + T);   // per wave
+    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_y + T + kWaves * RPW * 6);
 
     const int t = threadIdx.x;
-    const int wave = t / kWave;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
     const int lane = t % kWave;
     const int rb = (int)(blockIdx.x % (uint32_t)args.row_blocks);
     const int sp = (int)(blockIdx.x / (uint32_t)args.row_blocks);
@@ -226,48 +319,22 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     const int na = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_a + 1] - oa);
     const int64_t ob = args.cam_offs[(int64_t)s * args.n_cams + cam_b];
     const int nb = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_b + 1] - ob);
-    const int row0 = rb * kWaves * RPW;
+    const int row0 = rb * args.rows_per_wg;
     if (row0 >= na) return;   // uniform over the workgroup
 
     double f[9];
 #pragma unroll
     for (int k = 0; k < 9; ++k) f[k] = args.F[(int64_t)sp * 9 + k];
 
-    // Row lines of this workgroup's rows (one thread per row).
-    if (t < kWaves * RPW) {
-        const int i = row0 + t;
-        double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
-        bool deg = true;
-        if (i < na) {
-            x = args.pts[2 * (oa + i)];
-            y = args.pts[2 * (oa + i) + 1];
-            deg = row_line(f, x, y, l0, l1, l2);
-        }
-        s_row[t][0] = l0;
-        s_row[t][1] = l1;
-        s_row[t][2] = l2;
-        s_row[t][3] = x;
-        s_row[t][4] = y;
-        s_row[t][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
-    }
-
     const int64_t doff = args.dist_offs ? args.dist_offs[sp] : (int64_t)sp * args.mat_stride;
     const int64_t ld = args.ld ? args.ld : nb;
-    OutT *dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
-    const bool vec_ok = ((doff & 3) == 0) && ((ld & 3) == 0);
+    OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
+    const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
 
-    uint32_t bkey[RPW];
-    int32_t bidx[RPW];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-        bkey[r] = kKeyInvalid;
-        bidx[r] = 0x7FFFFFFF;
-    }
-
-    for (int c0 = 0; c0 < nb; c0 += kChunk) {
-        __syncthreads();   // row records visible / previous chunk consumed
-        {
-            const int j = c0 + t;
+    // column lines of columns [c0, c0 + T) -> LDS (threads stride the tile)
+    auto load_tile = [&](int c0) {
+        for (int jj = t; jj < T; jj += kThreads) {
+            const int j = c0 + jj;
             uint32_t st = kNone;
             double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
             if (j < nb) {
@@ -275,64 +342,123 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 y = args.pts[2 * (ob + j) + 1];
                 st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
             }
-            s_col[0][t] = l0;
-            s_col[1][t] = l1;
-            s_col[2][t] = l2;
-            s_col[3][t] = x;
-            s_col[4][t] = y;
-            s_cstate[t] = st;
+            s_l0[jj] = l0;
+            s_l1[jj] = l1;
+            s_l2[jj] = l2;
+            s_x[jj] = x;
+            s_y[jj] = y;
+            s_cst[jj] = st;
         }
+    };
+    const int n_tiles = (nb + T - 1) / T;
+    if (n_tiles == 1) {
+        load_tile(0);
         __syncthreads();
-
-        ColRegs c;
-        bool clean = true;
-#pragma unroll
-        for (int q = 0; q < kColsPerLane; ++q) {
-            const int jj = kColsPerLane * lane + q;
-            c.l0[q] = s_col[0][jj];
-            c.l1[q] = s_col[1][jj];
-            c.l2[q] = s_col[2][jj];
-            c.x[q] = s_col[3][jj];
-            c.y[q] = s_col[4][jj];
-            c.state[q] = s_cstate[jj];
-            clean &= (c.state[q] == kOk);
-        }
-        const int jbase = c0 + kColsPerLane * lane;
-        const bool fast = vec_ok && __all(clean);   // wave-uniform
-
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int lr = wave * RPW + r;
-            const int i = row0 + lr;
-            if (i >= na) break;   // uniform over the wave
-            const double rl0 = s_row[lr][0], rl1 = s_row[lr][1], rl2 = s_row[lr][2];
-            const double rx = s_row[lr][3], ry = s_row[lr][4];
-            // row state is uniform: one scalar branch per row, none per pair
-            const uint32_t rstate = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_row[lr][5]);
-            OutT *drow = dbase ? dbase + (int64_t)i * ld : nullptr;
-            if (fast && rstate == kOk) {
-                sweep_row<false, ARGMIN>(c, rl0, rl1, rl2, rx, ry, false, drow, jbase, nb, bkey[r],
-                                         bidx[r]);
-            } else {
-                // degenerate row line: d2 = 9999 for the whole row
-                sweep_row<true, ARGMIN>(c, rl0, rl1, rl2, rx, ry, rstate == kDeg, drow, jbase, nb,
-                                        bkey[r], bidx[r]);
-            }
-        }
     }
 
-    if (ARGMIN && args.row_offs) {
-        const int64_t roff = args.row_offs[sp];
+    const int wg_rows = min(args.rows_per_wg, na - row0);
+    const int n_groups = (wg_rows + kWaves * RPW - 1) / (kWaves * RPW);   // uniform over the WG
+    for (int g = 0; g < n_groups; ++g) {
+        const int grow0 = row0 + (g * kWaves + wave) * RPW;   // this wave's first row
+        const int nrows = min(RPW, min(na, row0 + wg_rows) - grow0);   // scalar, may be <= 0
+        if (lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
+            const int i = grow0 + lane;
+            double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+            bool deg = true;
+            if (lane < nrows) {
+                x = args.pts[2 * (oa + i)];
+                y = args.pts[2 * (oa + i) + 1];
+                deg = row_line(f, x, y, l0, l1, l2);
+            }
+            s_row[wave][lane][0] = l0;
+            s_row[wave][lane][1] = l1;
+            s_row[wave][lane][2] = l2;
+            s_row[wave][lane][3] = x;
+            s_row[wave][lane][4] = y;
+            s_row[wave][lane][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
+        }
+        // the same wave reads them back (LDS executes one wave's ops in order)
+        const bool rows_fast =
+            (nrows == RPW) && __all(lane >= RPW || s_row[wave][lane % RPW][5] == 0.0);
+
+        Best best[RPW];
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int i = row0 + wave * RPW + r;
-            if (i >= na) break;
-            uint32_t kmin;
-            int32_t imin;
-            wave_argmin(bkey[r], bidx[r], kmin, imin);
-            if (lane == 0) {
-                if (args.argmin) args.argmin[roff + i] = (kmin == kKeyInvalid) ? -1 : imin;
-                if (args.minval) args.minval[roff + i] = value_of_key(kmin);
+        for (int r = 0; r < RPW; ++r) best[r] = Best{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+
+        for (int tile = 0; tile < n_tiles; ++tile) {
+            if (n_tiles > 1) {   // large views: stream the column lines tile by tile
+                __syncthreads();
+                load_tile(tile * T);
+                __syncthreads();
+            }
+            const int tile_cols = min(T, nb - tile * T);
+            if (nrows <= 0) continue;
+            for (int c0 = 0; c0 < tile_cols; c0 += kChunk) {
+                ColRegs c;
+                bool clean = true;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = c0 + kColsPerLane * lane + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
+                    c.state[q] = s_cst[jj];
+                    clean &= (c.state[q] == kOk);
+                }
+                const int jbase = tile * T + c0 + kColsPerLane * lane;
+                const bool fast = rows_fast && __all(clean);   // wave-uniform
+                if (fast && vec_ok) {   // the common case: clean rows, aligned output
+                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast<ARGMIN, true>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                               s_row[wave][r][2], s_row[wave][r][3],
+                                               s_row[wave][r][4], reinterpret_cast<OutT *>(rp),
+                                               jbase, best[r]);
+                        rp += rstep;
+                        // keep the row address a running scalar: stops LICM
+                        // hoisting all RPW row bases out of the chunk loop
+                        // (they would be spilled to VGPR lanes)
+                        __asm__ volatile("" : "+s"(rp));
+                    }
+                } else if (fast && !dbase) {   // association only, no matrix output
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast<ARGMIN, false, OutT>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                                      s_row[wave][r][2], s_row[wave][r][3],
+                                                      s_row[wave][r][4], nullptr, jbase, best[r]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        if (r < nrows) {
+                            OutT *drow = dbase ? dbase + (int64_t)(grow0 + r) * ld : nullptr;
+                            const bool rdeg = __builtin_amdgcn_readfirstlane(
+                                                  (int)s_row[wave][r][5]) == (int)kDeg;
+                            row_safe<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                             s_row[wave][r][2], s_row[wave][r][3],
+                                             s_row[wave][r][4], rdeg, drow, jbase, nb, best[r]);
+                        }
+                    }
+                }
+            }
+        }
+
+        if (ARGMIN && args.row_offs && nrows > 0) {
+            const int64_t roff = args.row_offs[sp];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                if (r < nrows) {
+                    uint32_t kmin;
+                    int32_t imin;
+                    wave_argmin(best_key(best[r]), best[r].j, kmin, imin);
+                    if (lane == 0) {
+                        if (args.argmin) args.argmin[roff + grow0 + r] = (kmin == kKeyInvalid) ? -1 : imin;
+                        if (args.minval) args.minval[roff + grow0 + r] = value_of_key(kmin);
+                    }
+                }
             }
         }
     }
@@ -443,8 +569,22 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
     }
 }
 
+// ------------------------------------------------------- write probe ----
+// Speed-of-light reference for the roofline: every workgroup writes one
+// contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
+// wave instruction 1 KiB contiguous) -- the store form of the residual kernels.
+__global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_t n16, float val) {
+    const f32x4 v = {val, val, val, val};
+    const size_t base = (size_t)blockIdx.x * (4 * kThreads) + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const size_t i = base + (size_t)k * kThreads;
+        if (i < n16) __builtin_nontemporal_store(v, dst + i);
+    }
+}
+
 // ------------------------------------------------------------ host side ----
-constexpr int kRowsPerWave = 16;       // pairwise: 64 rows per workgroup
+constexpr int kRowsPerWave = 16;       // pairwise default: 64 rows per workgroup
 constexpr int kTripletRowsPerWave = 8; // triplet: 32 (i, j) rows per workgroup
 
 thread_local char g_err[512];
@@ -484,26 +624,62 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
     return MVM_OK;
 }
 
-int64_t grid_blocks(int64_t units, int64_t per_unit) { return units * per_unit; }
+constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 
-int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, bool argmin,
-                           bool f64, hipStream_t stream) {
-    if (n_scenes < 0 || max_rows < 0)
-        return fail(MVM_ERR_INVALID_ARGUMENT, "negative n_scenes/max_rows");
+template <int RPW>
+size_t pairwise_lds_bytes(int col_tile) {
+    return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
+           (size_t)kWaves * RPW * 6 * sizeof(double);
+}
+
+template <int RPW>
+void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_cols,
+                         int row_groups, bool argmin, bool f64, hipStream_t stream) {
+    a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
+    a.rows_per_wg = kWaves * RPW * row_groups;
+    a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
+    const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile);
+    if (f64) {
+        pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
+    } else if (argmin) {
+        pairwise_kernel<RPW, true, float><<<grid, block, lds, stream>>>(a);
+    } else {
+        pairwise_kernel<RPW, false, float><<<grid, block, lds, stream>>>(a);
+    }
+}
+
+// Tuning knobs (read per launch; defaults tuned on MI355X):
+//   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
+//   MVM_PAIRWISE_RG   row groups per wave (1..16)
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int32_t max_cols,
+                           bool argmin, bool f64, hipStream_t stream) {
+    if (n_scenes < 0 || max_rows < 0 || max_cols < 0)
+        return fail(MVM_ERR_INVALID_ARGUMENT, "negative n_scenes/max_rows/max_cols");
     if (n_scenes == 0 || max_rows == 0) return MVM_OK;
-    const int rows_per_wg = kWaves * kRowsPerWave;
-    a.row_blocks = (max_rows + rows_per_wg - 1) / rows_per_wg;
-    const int64_t blocks = grid_blocks((int64_t)n_scenes * a.n_pairs, a.row_blocks);
+    int rpw = env_int("MVM_PAIRWISE_RPW", kRowsPerWave);
+    if (rpw != 4 && rpw != 8 && rpw != 16) rpw = kRowsPerWave;
+    // enough row groups to amortise the column lines over >= ~256 rows, but
+    // never more than the rows a view has
+    const int groups_needed = (max_rows + kWaves * rpw - 1) / (kWaves * rpw);
+    int rg = env_int("MVM_PAIRWISE_RG", 0);
+    if (rg <= 0) rg = max(1, min(groups_needed, 256 / (kWaves * rpw)));
+    rg = max(1, min(rg, 16));
+    const int64_t sp_count = (int64_t)n_scenes * a.n_pairs;
+    const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
+    const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
     if (blocks > 0x7FFFFFFFLL)
         return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                     (long long)blocks);
-    const dim3 grid((unsigned)blocks), block(kThreads);
-    if (f64) {
-        pairwise_kernel<kRowsPerWave, false, double><<<grid, block, 0, stream>>>(a);
-    } else if (argmin) {
-        pairwise_kernel<kRowsPerWave, true, float><<<grid, block, 0, stream>>>(a);
-    } else {
-        pairwise_kernel<kRowsPerWave, false, float><<<grid, block, 0, stream>>>(a);
+    switch (rpw) {
+    case 4: launch_pairwise_rpw<4>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
+    case 8: launch_pairwise_rpw<8>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
+    default: launch_pairwise_rpw<16>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
     }
     return check_launch("pairwise_kernel");
 }
@@ -531,14 +707,14 @@ const char *mvm_status_string(int status) {
 int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                                  const double *F_dev, const int32_t *pair_a,
                                  const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
-                                 int32_t n_pairs, int32_t max_rows, const int64_t *dist_offs_dev,
+                                 int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
                                  const int64_t *row_offs_dev, float *dist_dev,
                                  int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream) {
     g_err[0] = 0;
     PairArgs a{};
     int st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
     if (st) return st;
-    if (n_scenes > 0 && max_rows > 0 && (!pts_dev || !cam_offs_dev || !F_dev))
+    if (n_scenes > 0 && max_n > 0 && (!pts_dev || !cam_offs_dev || !F_dev))
         return fail(MVM_ERR_INVALID_ARGUMENT, "null input pointer");
     if (dist_dev && !dist_offs_dev) return fail(MVM_ERR_INVALID_ARGUMENT, "dist without dist_offs");
     if ((argmin_dev || minval_dev) && !row_offs_dev)
@@ -553,20 +729,20 @@ int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_
     a.minval = minval_dev;
     a.ld = 0;
     const bool want_argmin = argmin_dev || minval_dev;
-    return launch_pairwise_common(a, n_scenes, max_rows, want_argmin, false,
+    return launch_pairwise_common(a, n_scenes, max_n, max_n, want_argmin, false,
                                   reinterpret_cast<hipStream_t>(stream));
 }
 
 int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev,
                               const double *F_dev, const int32_t *pair_a, const int32_t *pair_b,
                               int32_t n_scenes, int32_t n_cams, int32_t n_pairs,
-                              int32_t max_rows, int64_t mat_stride, int64_t ld, double *e_dev,
+                              int32_t max_n, int64_t mat_stride, int64_t ld, double *e_dev,
                               mvm_stream_t stream) {
     g_err[0] = 0;
     PairArgs a{};
     int st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
     if (st) return st;
-    if (n_scenes > 0 && max_rows > 0 && (!pts_dev || !cam_offs_dev || !F_dev || !e_dev))
+    if (n_scenes > 0 && max_n > 0 && (!pts_dev || !cam_offs_dev || !F_dev || !e_dev))
         return fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     if (ld <= 0 || mat_stride < 0)
         return fail(MVM_ERR_INVALID_ARGUMENT, "ld must be > 0 and mat_stride >= 0");
@@ -576,8 +752,21 @@ int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev
     a.dist = e_dev;
     a.mat_stride = mat_stride;
     a.ld = ld;
-    return launch_pairwise_common(a, n_scenes, max_rows, false, true,
+    return launch_pairwise_common(a, n_scenes, max_n, max_n, false, true,
                                   reinterpret_cast<hipStream_t>(stream));
+}
+
+int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
+    g_err[0] = 0;
+    if (!dst_dev || (((uintptr_t)dst_dev) & 15) || (bytes & 15))
+        return fail(MVM_ERR_INVALID_ARGUMENT, "write probe needs a 16-byte aligned buffer/size");
+    const size_t n16 = bytes / 16;
+    const size_t blocks = (n16 + 4 * kThreads - 1) / (4 * kThreads);
+    if (blocks == 0) return MVM_OK;
+    if (blocks > 0x7FFFFFFFull) return fail(MVM_ERR_UNSUPPORTED, "write probe buffer too large");
+    write_probe_kernel<<<(unsigned)blocks, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<f32x4 *>(dst_dev), n16, 1.0f);
+    return check_launch("write_probe_kernel");
 }
 
 size_t mvm_triplet_workspace_bytes(int32_t n_scenes, int32_t max_n) {

@@ -27,6 +27,7 @@ from . import _native
 __all__ = [
     "PairwisePlan", "TripletPlan",
     "pairwise_residual_argmin", "pairwise_residual_f64", "triplet_cost_argmin",
+    "hbm_write_probe",
 ]
 
 
@@ -68,7 +69,7 @@ def _check_inputs(pts: Tensor, cam_offs: Tensor, F: Tensor, n_views: int, n_mats
 @torch.library.custom_op("mvmatch::pairwise_residual_argmin_out",
                          mutates_args=("dist", "argmin", "minval"))
 def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: List[int],
-                                 pair_b: List[int], n_scenes: int, n_cams: int, max_rows: int,
+                                 pair_b: List[int], n_scenes: int, n_cams: int, max_n: int,
                                  dist_offs: Tensor, row_offs: Tensor, dist: Tensor,
                                  argmin: Tensor, minval: Tensor) -> None:
     n_pairs = len(pair_a)
@@ -80,20 +81,20 @@ def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_
     pa = (ctypes.c_int32 * n_pairs)(*pair_a)
     pb = (ctypes.c_int32 * n_pairs)(*pair_b)
     st = _native.load().mvm_pairwise_residual_argmin(
-        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_rows,
+        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_n,
         _p(dist_offs), _p(row_offs), _p(dist), _p(argmin), _p(minval), _stream(pts))
     _native.check("mvm_pairwise_residual_argmin", st)
 
 
 @pairwise_residual_argmin_out.register_fake
-def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_rows, dist_offs, row_offs, dist,
+def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_n, dist_offs, row_offs, dist,
       argmin, minval):
     return None
 
 
 @torch.library.custom_op("mvmatch::pairwise_residual_f64_out", mutates_args=("e",))
 def pairwise_residual_f64_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: List[int],
-                              pair_b: List[int], n_scenes: int, n_cams: int, max_rows: int,
+                              pair_b: List[int], n_scenes: int, n_cams: int, max_n: int,
                               mat_stride: int, ld: int, e: Tensor) -> None:
     n_pairs = len(pair_a)
     _check_inputs(pts, cam_offs, F, n_scenes * n_cams, n_scenes * n_pairs)
@@ -103,13 +104,13 @@ def pairwise_residual_f64_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: 
     pa = (ctypes.c_int32 * n_pairs)(*pair_a)
     pb = (ctypes.c_int32 * n_pairs)(*pair_b)
     st = _native.load().mvm_pairwise_residual_f64(
-        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_rows, mat_stride,
+        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_n, mat_stride,
         ld, _p(e), _stream(pts))
     _native.check("mvm_pairwise_residual_f64", st)
 
 
 @pairwise_residual_f64_out.register_fake
-def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_rows, mat_stride, ld, e):
+def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_n, mat_stride, ld, e):
     return None
 
 
@@ -160,6 +161,7 @@ class PairwisePlan:
         self.pair_b = [int(b) for b in pairs[:, 1]]
         self.max_rows = int(na.max()) if na.size else 0
         self.max_cols = int(nb.max()) if nb.size else 0
+        self.max_n = max(self.max_rows, self.max_cols)
         self.na, self.nb = na, nb
         self.n_dist = int(dist_offs[-1])
         self.n_rows = int(row_offs[-1])
@@ -188,7 +190,7 @@ def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: Pai
     else:
         dist, argmin, minval = out
     torch.ops.mvmatch.pairwise_residual_argmin_out(
-        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_rows,
+        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_n,
         plan.dist_offs, plan.row_offs, dist, argmin, minval)
     return dist, argmin, minval
 
@@ -200,7 +202,7 @@ def pairwise_residual_f64(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: Pairwi
     e = torch.zeros(plan.n_scenes * len(plan.pair_a) * rows * ld, dtype=torch.float64,
                     device=pts.device)
     torch.ops.mvmatch.pairwise_residual_f64_out(
-        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_rows,
+        pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_n,
         rows * ld, ld, e)
     return e.view(plan.n_scenes * len(plan.pair_a), rows, ld)
 
@@ -246,3 +248,12 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
         pts, cam_offs, F, plan.n_scenes, plan.max_n, plan.cube_offs, plan.row_offs, cube, argmin,
         minval, plan.workspace)
     return cube, argmin, minval
+
+
+def hbm_write_probe(buf: Tensor) -> None:
+    """Stream 16-byte nontemporal stores over ``buf`` (roofline reference)."""
+    if buf.device.type != "cuda" or not buf.is_contiguous():
+        raise ValueError("hbm_write_probe needs a contiguous GPU tensor")
+    nbytes = buf.numel() * buf.element_size() // 16 * 16
+    st = _native.load().mvm_hbm_write_probe(_p(buf), nbytes, _stream(buf))
+    _native.check("mvm_hbm_write_probe", st)

@@ -72,13 +72,14 @@ const char *mvm_status_string(int status);
  *   minval_dev[...]                         = e[i][argmin] (NaN if n_b == 0)
  * dist_dev, argmin_dev and minval_dev may each be NULL (not produced).
  * pair_a / pair_b are HOST arrays of n_pairs camera indices (a != b).
- * max_rows is a host-known upper bound on n_a over all (scene, pair): it only
- * sizes the grid (rows beyond the real n_a are skipped on the device).
+ * max_n is a host-known upper bound on every view's detection count (n_a and
+ * n_b over all (scene, pair)): it sizes the grid and the LDS column tile;
+ * rows/columns beyond the real counts are skipped on the device.
  */
 int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                                  const double *F_dev, const int32_t *pair_a,
                                  const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
-                                 int32_t n_pairs, int32_t max_rows, const int64_t *dist_offs_dev,
+                                 int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
                                  const int64_t *row_offs_dev, float *dist_dev,
                                  int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream);
 
@@ -92,7 +93,7 @@ int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_
 int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev,
                               const double *F_dev, const int32_t *pair_a, const int32_t *pair_b,
                               int32_t n_scenes, int32_t n_cams, int32_t n_pairs,
-                              int32_t max_rows, int64_t mat_stride, int64_t ld, double *e_dev,
+                              int32_t max_n, int64_t mat_stride, int64_t ld, double *e_dev,
                               mvm_stream_t stream);
 
 /*
@@ -113,6 +114,14 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                             const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                             float *cube_dev, int32_t *argmin_dev, float *minval_dev,
                             void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream);
+
+/*
+ * Diagnostic: fill `bytes` (multiple of 16, 16-byte aligned) of device memory
+ * with the same 16-byte nontemporal store stream the residual kernels use.
+ * bench.py times it to report the achievable HBM write bandwidth next to the
+ * kernels' roofline fraction.
+ */
+int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream);
 
 #ifdef __cplusplus
 }
