@@ -1,0 +1,98 @@
+"""The C ABI library: loads without a GPU, exports every symbol the header
+declares, and its host-side validation returns the documented status codes
+(no compute calls here -- those are the -m gpu tests)."""
+import ctypes
+
+import pytest
+
+from bpc_baseline_amd import _native
+
+
+@pytest.fixture(scope="module")
+def lib():
+    return _native.load()
+
+
+def test_header_symbols_exported(lib):
+    names = _native.header_symbols()
+    assert len(names) >= 8
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/mvmatch.h but not exported"
+    assert set(names) == set(_native.SIGNATURES), "ctypes signature table out of sync with header"
+
+
+def test_version_and_status_strings(lib):
+    assert _native.version().startswith("mvmatch ")
+    assert "gfx950" in _native.version()
+    assert lib.mvm_status_string(0) == b"ok"
+    assert lib.mvm_status_string(3) == b"workspace too small"
+
+
+def _pairs(*ab):
+    n = len(ab)
+    return (ctypes.c_int32 * n)(*[a for a, _ in ab]), (ctypes.c_int32 * n)(*[b for _, b in ab])
+
+
+FAKE = ctypes.c_void_p(0x1000)   # never dereferenced: validation fails first
+
+
+def test_unsupported_camera_count(lib):
+    pa, pb = _pairs((0, 1))
+    st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 99, 1, 4,
+                                          FAKE, FAKE, FAKE, FAKE, FAKE, None)
+    assert st == 2
+    assert b"n_cams" in lib.mvm_last_error_string()
+
+
+def test_bad_pair_index(lib):
+    pa, pb = _pairs((0, 3))
+    st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 3, 1, 4,
+                                          FAKE, FAKE, FAKE, FAKE, FAKE, None)
+    assert st == 1
+    pa, pb = _pairs((1, 1))
+    assert lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 3, 1, 4,
+                                            FAKE, FAKE, FAKE, FAKE, FAKE, None) == 1
+
+
+def test_outputs_need_offsets(lib):
+    pa, pb = _pairs((0, 1))
+    st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 2, 1, 4,
+                                          None, FAKE, FAKE, None, None, None)
+    assert st == 1 and b"dist_offs" in lib.mvm_last_error_string()
+    st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 2, 1, 4,
+                                          FAKE, None, None, FAKE, None, None)
+    assert st == 1 and b"row_offs" in lib.mvm_last_error_string()
+
+
+def test_empty_batch_is_a_noop(lib):
+    pa, pb = _pairs((0, 1))
+    # zero scenes / zero detections: nothing is launched, status ok
+    assert lib.mvm_pairwise_residual_argmin(None, None, None, pa, pb, 0, 2, 1, 0,
+                                            None, None, None, None, None, None) == 0
+    assert lib.mvm_triplet_cost_argmin(None, None, None, 0, 0, None, None, None, None, None,
+                                       None, 0, None) == 0
+
+
+def test_triplet_workspace_contract(lib):
+    need = lib.mvm_triplet_workspace_bytes(10, 30)
+    assert need == 10 * 3 * 30 * 32 * 8          # ld rounded up to a multiple of 4
+    assert lib.mvm_triplet_workspace_bytes(0, 30) == 0
+    st = lib.mvm_triplet_cost_argmin(FAKE, FAKE, FAKE, 10, 30, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                     FAKE, need - 16, None)
+    assert st == 3
+    st = lib.mvm_triplet_cost_argmin(FAKE, FAKE, FAKE, 10, 30, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                     ctypes.c_void_p(0x1004), need, None)
+    assert st == 1   # misaligned workspace
+
+
+def test_write_probe_validation(lib):
+    assert lib.mvm_hbm_write_probe(None, 1024, None) == 1
+    assert lib.mvm_hbm_write_probe(FAKE, 1000, None) == 1
+
+
+def test_check_raises(lib):
+    with pytest.raises(_native.MvmError):
+        pa, pb = _pairs((0, 1))
+        st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 99, 1, 4,
+                                              FAKE, FAKE, FAKE, FAKE, FAKE, None)
+        _native.check("mvm_pairwise_residual_argmin", st)

@@ -1,0 +1,130 @@
+"""Host-side logic (CPU): plans, synthetic generator, sharding, input
+validation, the 'no CPU path' contract, and the float32-exactness claim of
+the kernel's exponent-decrement halving."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+
+
+def test_pairwise_plan_offsets_match_oracle():
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(7, 4, 33, seed=2, ragged=True)
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu")
+    doff, roff = O.pairwise_offsets(b.cam_offs, b.n_scenes, b.n_cams, b.pairs)
+    assert np.array_equal(plan.dist_offs_host, doff) and np.array_equal(plan.row_offs_host, roff)
+    assert plan.n_dist == b.n_residual_pairs()
+    assert plan.max_n == int(b.counts().max())
+
+
+def test_triplet_plan_offsets():
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(5, 3, 20, seed=3, ragged=True)
+    plan = ops.TripletPlan(b.cam_offs, b.n_scenes, device="cpu")
+    coff, roff = O.cube_offsets(b.cam_offs, b.n_scenes)
+    assert np.array_equal(plan.cube_offs_host, coff) and np.array_equal(plan.row_offs_host, roff)
+    assert plan.workspace.numel() >= plan.workspace_bytes
+
+
+def test_synth_is_deterministic_and_shardable():
+    from bpc_baseline_amd.synth import make_scenes
+    full = make_scenes(6, 3, 16, seed=11)
+    tail = make_scenes(3, 3, 16, seed=11, first_scene=3)
+    assert np.array_equal(full.F[3 * 3:], tail.F)
+    assert np.array_equal(full.pts[full.cam_offs[9]:], tail.pts)
+    again = make_scenes(6, 3, 16, seed=11)
+    assert np.array_equal(full.pts, again.pts)
+
+
+def test_synth_centroids_are_half_integers():
+    """_detect truncates box corners to int and averages (process_pose.py:134-136)."""
+    from bpc_baseline_amd.synth import make_scenes, make_capture
+    b = make_scenes(3, 4, 50, seed=5)
+    assert np.all(2 * b.pts == np.round(2 * b.pts))
+    _, _, dets = make_capture(np.random.default_rng(0), 3, 5)
+    for d in dets[0]:
+        x1, y1, x2, y2 = d["bbox"]
+        assert all(isinstance(v, int) for v in d["bbox"])
+        assert d["bb_center"] == (0.5 * (x1 + x2), 0.5 * (y1 + y2))
+
+
+def test_synth_true_matches_have_low_cost():
+    """Sanity of the synthetic rig: real objects match below the reference's
+    threshold of 30 px while clutter does not."""
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(1, 3, 64, seed=8)
+    _, am, mv, _, _ = O.cube(b.pts, b.cam_offs, b.F, 1)
+    assert np.sum(mv < 30) >= 16
+    assert np.median(mv) > 30
+
+
+def test_shard_range_partitions():
+    from bpc_baseline_amd.distributed import shard_range
+    for n in (0, 1, 7, 10000, 10001):
+        for w in (1, 2, 3, 8):
+            parts = [shard_range(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+            sizes = [b - a for a, b in parts]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def test_ops_reject_cpu_tensors():
+    """The matcher has no CPU path: host tensors are refused loudly."""
+    from bpc_baseline_amd import ops
+    plan = ops.PairwisePlan(np.array([0, 1, 2], np.int64), 1, 2, [[0, 1]], device="cpu")
+    with pytest.raises(ValueError, match="GPU"):
+        ops.pairwise_residual_argmin(torch.zeros(2, 2, dtype=torch.float64),
+                                     torch.tensor([0, 1, 2]), torch.zeros(9, dtype=torch.float64),
+                                     plan)
+
+
+@pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
+def test_dropin_fails_loudly_without_gpu():
+    from bpc_baseline_amd.inference import epipolar_matching as em
+    with pytest.raises(RuntimeError, match="GPU"):
+        em.epipolar_error((1.0, 2.0), (3.0, 4.0), np.eye(3))
+    d = [{"bb_center": (1.0, 2.0), "bbox": (0, 0, 2, 4)}]
+    with pytest.raises(RuntimeError, match="GPU"):
+        em.compute_cost_matrix(d, d, d, np.eye(3), np.eye(3), np.eye(3))
+
+
+def test_dropin_empty_view_returns_zero_cube():
+    """N == 0 (or M, P): the reference loop never runs -> zeros((N, M, P)) float32.
+    Needs no GPU (matches the reference exactly without launching)."""
+    from bpc_baseline_amd.inference import epipolar_matching as em
+    d = [{"bb_center": (1.0, 2.0), "bbox": (0, 0, 2, 4)}] * 3
+    c = em.compute_cost_matrix([], d, d, np.eye(3), np.eye(3), np.eye(3))
+    assert c.shape == (0, 3, 3) and c.dtype == np.float32
+    c = em.compute_cost_matrix(d, d, [], np.eye(3), np.eye(3), np.eye(3))
+    assert c.shape == (3, 3, 0)
+
+
+def _half_for_f32_np(s):
+    """numpy emulation of the kernel's half_for_f32 (mvm_kernels.hip)."""
+    b = s.view(np.uint64)
+    hi = (b >> np.uint64(32)).astype(np.int64)
+    hi = np.maximum(hi - 0x00100000, 0).astype(np.uint64)
+    return ((hi << np.uint64(32)) | (b & np.uint64(0xFFFFFFFF))).view(np.float64)
+
+
+def test_exponent_halving_is_exact_after_f32_cast():
+    """float32(half_for_f32(s)) == float32(0.5 * s) for every s >= +0 finite:
+    random mantissas over all binades, every binade boundary, subnormals, 0."""
+    rng = np.random.default_rng(0)
+    exps = np.arange(-1074, 1024)
+    mant = rng.uniform(1.0, 2.0, size=exps.size * 64)
+    s = np.ldexp(mant, np.repeat(exps, 64))
+    s = s[np.isfinite(s)]
+    edges = np.ldexp(1.0, np.arange(-1074, 1023)).astype(np.float64)
+    extra = np.concatenate([edges, np.nextafter(edges, 0), np.nextafter(edges, np.inf),
+                            [0.0, 5e-324, 2.2250738585072014e-308, 4.450147717014403e-308,
+                             np.finfo(np.float64).max / 4]])
+    s = np.concatenate([s, extra]).astype(np.float64)
+    with np.errstate(over="ignore", under="ignore"):
+        want = (0.5 * s).astype(np.float32)
+        got = _half_for_f32_np(s.copy()).astype(np.float32)
+    assert np.array_equal(want.view(np.int32), got.view(np.int32))
