@@ -569,6 +569,168 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
     }
 }
 
+// ------------------------------------------------- fast triplet kernel ----
+// float32(RN(x / 3)) for x >= +0 without an IEEE division in the common case.
+// q0 = RN(x * RN(1/3)) is within one ulp of RN(x / 3) (RN(1/3) = (1 - 2^-54)/3,
+// so |x*RN(1/3) - x/3| <= ulp/2, plus the product's own rounding).  Their
+// float32 roundings can differ only if a float32 rounding midpoint -- an fp64
+// value whose low 29 mantissa bits are exactly 2^28 -- lies within one ulp of
+// q0, or if the result leaves the float32 normal range.  Those (rare) lanes
+// take the correctly rounded division; tests/test_host_logic.py checks the
+// rule on random and adversarial near-midpoint inputs.
+constexpr double kThird = 1.0 / 3.0;
+
+// 4 consecutive doubles at a 16-byte aligned address (two dwordx4 loads);
+// lanes past the view's end read zeros.
+__device__ __forceinline__ void load4(const double *p, int valid, double out[4]) {
+    if (valid >= 4) {
+        const f64x2 lo = *reinterpret_cast<const f64x2 *>(p);
+        const f64x2 hi = *reinterpret_cast<const f64x2 *>(p + 2);
+        out[0] = lo.x;
+        out[1] = lo.y;
+        out[2] = hi.x;
+        out[3] = hi.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[q] = q < valid ? p[q] : 0.0;
+    }
+}
+
+__device__ __forceinline__ bool third_fast_ok(double q0) {
+    const uint64_t b = (uint64_t)__double_as_longlong(q0);
+    const uint32_t lo = (uint32_t)b, hi = (uint32_t)(b >> 32);
+    const uint32_t low29 = lo & 0x1FFFFFFFu;
+    const bool near_mid = (low29 - ((1u << 28) - 3u)) <= 6u;      // |low29 - 2^28| <= 3
+    const bool in_range = ((hi >> 20) - (1023u - 126u)) <= 252u;   // 2^-126 <= q0 < 2^127
+    return !near_mid && in_range;                                  // NaN/inf/negative: false
+}
+
+// Three-camera cube for views with P <= 256 (one k chunk): lanes own 4
+// consecutive k; each wave owns RPW consecutive j and keeps e23[j][k] for
+// them in registers (8*RPW VGPRs), then sweeps i: e13[i][k] is one 32-byte
+// load per lane per i, e12[i][j] a scalar load, and every (i, j) row is one
+// 16-byte-per-lane coalesced store followed by a DPP argmin over k.
+// Workgroup = (scene, block of 4*RPW j's, slice of i).
+struct Cube256Args {
+    const int64_t *cam_offs;
+    const double *e;
+    int64_t mat_stride;
+    int64_t ld;
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t j_blocks, i_splits, i_chunk;
+};
+
+template <int RPW>
+__global__ __launch_bounds__(kThreads) void triplet256_kernel(Cube256Args args) {
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_splits);
+    const int s = (int)(blockIdx.x / per_scene);
+    const int rem = (int)(blockIdx.x % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int is = rem / args.j_blocks;
+    const int64_t c0 = args.cam_offs[3 * (int64_t)s];
+    const int N = (int)(args.cam_offs[3 * (int64_t)s + 1] - c0);
+    const int M = (int)(args.cam_offs[3 * (int64_t)s + 2] - args.cam_offs[3 * (int64_t)s + 1]);
+    const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
+    const int j0 = (jb * kWaves + wave) * RPW;
+    const int i_begin = is * args.i_chunk;
+    const int i_end = min(N, i_begin + args.i_chunk);
+    if (j0 >= M || i_begin >= N || P == 0) return;   // wave-uniform; no barriers below
+    const int nrows = min(RPW, M - j0);
+
+    const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
+    const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride;
+    const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
+    const int kb = kColsPerLane * lane;
+    bool kval[kColsPerLane];
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) kval[q] = kb + q < P;
+    const int64_t coff = args.cube_offs[s];
+    const bool fast_shape = (P == kChunk) && ((coff & 3) == 0) && args.cube;
+
+    const int kvalid = P - kb;   // valid columns of this lane (may be <= 0)
+    double a23[RPW][kColsPerLane];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+        load4(e23 + (int64_t)(j0 + min(r, nrows - 1)) * args.ld + kb, kvalid, a23[r]);
+
+    const int64_t roff = args.row_offs[s];
+    for (int i = i_begin; i < i_end; ++i) {
+        double a13[kColsPerLane];
+        load4(e13 + (int64_t)i * args.ld + kb, kvalid, a13);
+        // e12[i][j0 .. j0+RPW): the same 64 bytes for every lane (broadcast)
+        double a12[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; r += 2) {
+            const f64x2 v2 = *reinterpret_cast<const f64x2 *>(e12 + (int64_t)i * args.ld + j0 + r);
+            a12[r] = v2.x;
+            a12[r + 1] = v2.y;
+        }
+        uint32_t key[RPW];
+        int32_t idx[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            key[r] = kKeyInvalid;
+            idx[r] = 0x7FFFFFFF;
+            if (r >= nrows) continue;   // uniform
+            const double v12 = a12[r];
+            double sum[kColsPerLane], q0[kColsPerLane];
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                q0[q] = sum[q] * kThird;
+                ok &= third_fast_ok(q0[q]);
+            }
+            float v[kColsPerLane];
+            const int64_t row = (int64_t)i * M + j0 + r;
+            if (fast_shape && __all(ok)) {   // every lane valid, finite, fast division exact
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                              (uint32_t)kb * 4u, v);
+                Best b{v[0], kb};
+#pragma unroll
+                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                key[r] = __float_as_uint(b.v) + 1u;
+                idx[r] = b.j;
+            } else {
+                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    v[q] = (float)qq;
+                    if (kval[q]) {
+                        if (args.cube) __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                        best_update_safe(b, v[q], kb + q);
+                    }
+                }
+                key[r] = best_key(b);
+                idx[r] = b.j;
+            }
+        }
+        // batched per-row reductions (independent DPP chains interleave)
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            if (r >= nrows) continue;
+            uint32_t kmin;
+            int32_t imin;
+            wave_argmin(key[r], idx[r], kmin, imin);
+            if (lane == 0) {
+                const int64_t row = roff + (int64_t)i * M + j0 + r;
+                if (args.argmin) args.argmin[row] = (kmin == kKeyInvalid) ? -1 : imin;
+                if (args.minval) args.minval[row] = value_of_key(kmin);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------- write probe ----
 // Speed-of-light reference for the roofline: every workgroup writes one
 // contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
@@ -585,7 +747,8 @@ __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_
 
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;       // pairwise default: 64 rows per workgroup
-constexpr int kTripletRowsPerWave = 8; // triplet: 32 (i, j) rows per workgroup
+constexpr int kTripletRowsPerWave = 8; // generic triplet: 32 (i, j) rows per workgroup
+constexpr int kTriplet256RowsPerWave = 8;   // P <= 256 triplet: e23 rows held per wave
 
 thread_local char g_err[512];
 
@@ -799,6 +962,34 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     int st = mvm_pairwise_residual_f64(pts_dev, cam_offs_dev, F_dev, pa, pb, n_scenes, 3, 3,
                                        max_n, mat_stride, ld, (double *)workspace_dev, stream);
     if (st) return st;
+    if (max_n <= kChunk && env_int("MVM_TRIPLET_GENERIC", 0) == 0) {
+        // every P <= 256: register-resident e23 kernel
+        constexpr int rpw = kTriplet256RowsPerWave;
+        Cube256Args c{};
+        c.cam_offs = cam_offs_dev;
+        c.e = (const double *)workspace_dev;
+        c.mat_stride = mat_stride;
+        c.ld = ld;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.j_blocks = (max_n + kWaves * rpw - 1) / (kWaves * rpw);
+        // split i so the grid has >= ~4096 workgroups (>= 16 per CU)
+        const int64_t base = (int64_t)n_scenes * c.j_blocks;
+        const int64_t want = (4096 + base - 1) / base;
+        const int64_t cap = max_n / 8 > 1 ? max_n / 8 : 1;
+        const int splits = (int)(want < 1 ? 1 : (want > cap ? cap : want));
+        c.i_chunk = (max_n + splits - 1) / splits;
+        c.i_splits = (max_n + c.i_chunk - 1) / c.i_chunk;
+        const int64_t blocks = base * c.i_splits;
+        if (blocks > 0x7FFFFFFFLL)
+            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+        triplet256_kernel<rpw><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+        return check_launch("triplet256_kernel");
+    }
     CubeArgs c{};
     c.cam_offs = cam_offs_dev;
     c.e = (const double *)workspace_dev;

@@ -128,3 +128,36 @@ def test_exponent_halving_is_exact_after_f32_cast():
         want = (0.5 * s).astype(np.float32)
         got = _half_for_f32_np(s.copy()).astype(np.float32)
     assert np.array_equal(want.view(np.int32), got.view(np.int32))
+
+
+def _third_fast_ok_np(q0):
+    """numpy emulation of third_fast_ok (mvm_kernels.hip)."""
+    b = q0.view(np.uint64)
+    lo = (b & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    hi = (b >> np.uint64(32)).astype(np.uint32)
+    low29 = lo & np.uint32(0x1FFFFFFF)
+    near = (low29 - np.uint32((1 << 28) - 3)) <= np.uint32(6)
+    in_range = ((hi >> np.uint32(20)) - np.uint32(1023 - 126)) <= np.uint32(252)
+    return ~near & in_range
+
+
+def test_fast_division_by_three_rule():
+    """The cube kernel's float32(RN(x/3)) shortcut: wherever third_fast_ok
+    accepts q0 = x * RN(1/3), float32(q0) == float32(x / 3).  Random values over
+    many binades plus adversarial x placed within +-3 ulps of 3 * (float32
+    rounding midpoint)."""
+    rng = np.random.default_rng(7)
+    third = np.float64(1.0) / np.float64(3.0)
+    x = np.concatenate([np.exp(rng.uniform(np.log(1e-40), np.log(1e40), 1_000_000)),
+                        rng.uniform(0, 30000, 1_000_000), [0.0, 3.0, 9999.0, 29997.0]])
+    f = rng.uniform(0.01, 5000, 200_000).astype(np.float32)
+    mid = (f.astype(np.float64) + np.nextafter(f, np.float32(np.inf)).astype(np.float64)) / 2
+    adv = mid * 3
+    x = np.concatenate([x] + [adv + k * np.spacing(adv) for k in range(-3, 4)])
+    q0 = x * third
+    ok = _third_fast_ok_np(q0.copy())
+    with np.errstate(over="ignore", under="ignore"):
+        a = (x / 3.0).astype(np.float32).view(np.int32)
+        b = q0.astype(np.float32).view(np.int32)
+    assert not np.any((a != b) & ok)
+    assert ok[1_000_000:2_000_000].mean() > 0.999   # realistic costs take the fast path
