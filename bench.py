@@ -36,7 +36,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from bpc_baseline_amd import ops  # noqa: E402
-from bpc_baseline_amd.distributed import gather_rows, init_from_env, max_over_ranks  # noqa: E402
+from bpc_baseline_amd.distributed import (ChunkedRowGather, gather_rows, init_from_env,  # noqa: E402
+                                          max_over_ranks)
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -158,14 +159,18 @@ def cpu_baseline(batch, mode: str, target_s: float):
                       f"OpenMP x{threads} on {cpu_model()}"}
 
 
-def load_traffic(workload: str):
+def load_traffic(workload: str, scenes_per_launch: int):
+    """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json), only if it
+    was collected on this workload at this launch size."""
     path = os.path.join(REPO, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             rec = json.load(fh).get(workload)
-        return rec
     except (OSError, ValueError):
         return None
+    if not rec or int(rec.get("scenes_per_launch", -1)) != int(scenes_per_launch):
+        return None
+    return rec
 
 
 def main():
@@ -223,8 +228,17 @@ def main():
             ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan,
                                     out=(dist_buf[:c.units], am, mv))
 
+    # the single association gather (N > 1), in per-launch pieces that overlap
+    # the next launch's compute; ragged shards fall back to one gather at the end
+    overlap = True
+    try:
+        gatherer = ChunkedRowGather(env, (argmin, minval),
+                                    [(c.row_base, c.row_base + c.plan.n_rows) for c in chunks])
+    except ValueError:
+        gatherer, overlap = None, False
+
     def step(events=None):
-        for c in chunks:
+        for k, c in enumerate(chunks):
             if events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(stream)
@@ -233,6 +247,10 @@ def main():
                 events.append((e0, e1, c))
             else:
                 launch(c)
+            if overlap:
+                gatherer.issue(k)
+        if overlap:
+            return gatherer.finish()
         return gather_rows(env, argmin, minval)
 
     for _ in range(args.warmup):
@@ -298,7 +316,7 @@ def main():
     cpu = None
     if world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, wl["mode"], args.cpu_seconds)
-    traffic = load_traffic(args.workload)
+    traffic = load_traffic(args.workload, min(wl["chunk"], n_local))
     out = {
         "metric": METRIC if wl["mode"] == "pairwise" else "cost-cube triples/sec",
         "value": value,
@@ -319,8 +337,9 @@ def main():
             "n_scenes_total": n_local * world if args.scaling == "weak" else wl["n_scenes"],
             "scenes_per_launch": wl["chunk"], "launches_per_step": len(chunks),
             "units_per_gpu_step": units_local,
-            "parallelism": f"scene-sharded x{world}, one RCCL gather per step" if world > 1
-                           else "single GPU",
+            "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
+                            f"({env.backend}{', overlapped per launch' if overlap else ''})")
+                           if world > 1 else "single GPU",
         },
         "roofline": {
             "bound": "hbm",

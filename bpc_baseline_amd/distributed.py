@@ -18,14 +18,15 @@ from typing import List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
-__all__ = ["DistEnv", "init_from_env", "shard_range", "gather_rows", "max_over_ranks"]
+__all__ = ["DistEnv", "init_from_env", "shard_range", "gather_rows", "max_over_ranks",
+           "ChunkedRowGather"]
 
 
 class DistEnv:
     def __init__(self, rank: int, world: int, local_rank: int, device: torch.device,
-                 initialised: bool):
+                 initialised: bool, backend: Optional[str] = None):
         self.rank, self.world, self.local_rank = rank, world, local_rank
-        self.device, self.initialised = device, initialised
+        self.device, self.initialised, self.backend = device, initialised, backend
 
     @property
     def is_root(self) -> bool:
@@ -33,30 +34,37 @@ class DistEnv:
 
     def barrier(self) -> None:
         if self.initialised:
-            if self.device.type == "cuda":
+            if self.device.type == "cuda" and self.backend == "nccl":
                 dist.barrier(device_ids=[self.device.index])
             else:
                 dist.barrier()
 
 
 def init_from_env(backend: Optional[str] = None, use_gpu: bool = True) -> DistEnv:
-    """Initialise torch.distributed from torchrun's env (single process if absent)."""
+    """Initialise torch.distributed from torchrun's env (single process if absent).
+
+    One process per GPU: rank -> cuda:LOCAL_RANK.  ``backend`` defaults to
+    "nccl" (RCCL over xGMI on ROCm) for GPU ranks and "gloo" otherwise;
+    MVM_DIST_BACKEND overrides it (gloo rehearsals of several ranks on one
+    GPU map LOCAL_RANK onto the visible devices round-robin)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("MVM_DIST_BACKEND") or backend or ("nccl" if use_gpu else "gloo")
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        n_dev = torch.cuda.device_count()
+        index = local_rank % n_dev if (backend == "gloo" and n_dev) else local_rank
+        torch.cuda.set_device(index)
+        device = torch.device("cuda", index)
     else:
         device = torch.device("cpu")
     initialised = False
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = backend or ("nccl" if use_gpu else "gloo")
         kw = {"device_id": device} if (use_gpu and backend == "nccl") else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
         initialised = True
-    return DistEnv(rank, world, local_rank, device, initialised)
+    return DistEnv(rank, world, local_rank, device, initialised, backend)
 
 
 def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
@@ -72,6 +80,8 @@ def gather_rows(env: DistEnv, *tensors: torch.Tensor) -> Optional[List[torch.Ten
     Returns the gathered tensors on rank 0, None elsewhere; identity at world 1."""
     if not env.initialised:
         return list(tensors)
+    if env.backend == "gloo" and tensors[0].device.type != "cpu":
+        tensors = tuple(t.cpu() for t in tensors)   # gloo collectives run on host memory
     n_local = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=tensors[0].device)
     sizes = [torch.zeros_like(n_local) for _ in range(env.world)]
     dist.all_gather(sizes, n_local)
@@ -92,6 +102,58 @@ def gather_rows(env: DistEnv, *tensors: torch.Tensor) -> Optional[List[torch.Ten
 def max_over_ranks(env: DistEnv, value: float) -> float:
     if not env.initialised:
         return value
-    t = torch.tensor([value], dtype=torch.float64, device=env.device)
+    dev = env.device if env.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+class ChunkedRowGather:
+    """The association gather, split into pieces that overlap the compute.
+
+    Every rank holds its rows in equally laid-out buffers.  ``issue(k)``
+    enqueues an asynchronous gather of piece k to rank 0 right after the
+    launch that produced it: the collective (RCCL on its own stream) waits
+    only for work already enqueued on the compute stream, so piece k moves
+    over xGMI while piece k+1 computes.  ``finish()`` makes the compute
+    stream wait for every outstanding piece.  With world 1 it is a no-op.
+    Row counts must be equal on all ranks (checked once at construction).
+    """
+
+    def __init__(self, env: DistEnv, tensors, pieces):
+        self.env, self.tensors, self.pieces = env, list(tensors), list(pieces)
+        self.handles = []
+        self.recv = None
+        if not env.initialised:
+            return
+        n = torch.tensor([self.tensors[0].numel()], dtype=torch.int64,
+                         device=env.device if env.backend == "nccl" else "cpu")
+        sizes = [torch.zeros_like(n) for _ in range(env.world)]
+        dist.all_gather(sizes, n)
+        if len({int(x.item()) for x in sizes}) != 1:
+            raise ValueError("ChunkedRowGather needs the same row count on every rank")
+        if env.is_root:
+            self.recv = [torch.empty((env.world, t.numel()), dtype=t.dtype, device=t.device)
+                         for t in self.tensors]
+
+    def issue(self, k: int) -> None:
+        if not self.env.initialised:
+            return
+        a, b = self.pieces[k]
+        for i, t in enumerate(self.tensors):
+            src = t[a:b]
+            if self.env.backend == "gloo" and src.device.type != "cpu":
+                src = src.cpu()
+            dst = None
+            if self.env.is_root:
+                dst = [self.recv[i][r, a:b] for r in range(self.env.world)]
+                if self.env.backend == "gloo":
+                    dst = [d.cpu() for d in dst]
+            self.handles.append(dist.gather(src.contiguous(), gather_list=dst, dst=0,
+                                            async_op=True))
+
+    def finish(self):
+        for h in self.handles:
+            h.wait()
+        self.handles = []
+        return self.recv

@@ -54,3 +54,35 @@ def test_sharded_gather_equals_single_process(tmp_path, world):
     assert np.array_equal(np.load(tmp_path / "argmin.npy"), am)
     assert np.array_equal(np.load(tmp_path / "minval.npy").view(np.int32), mv.view(np.int32))
     assert float(np.load(tmp_path / "tmax.npy")[0]) == world
+
+
+def _chunked_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bpc_baseline_amd.distributed import init_from_env, ChunkedRowGather
+    env = init_from_env(backend="gloo", use_gpu=False)
+    n = 103
+    a = torch.arange(n, dtype=torch.int32) + 1000 * rank
+    m = torch.arange(n, dtype=torch.float32) * 0.5 + rank
+    pieces = [(0, 40), (40, 41), (41, 103)]
+    g = ChunkedRowGather(env, (a, m), pieces)
+    for k in range(len(pieces)):
+        g.issue(k)
+    recv = g.finish()
+    if env.is_root:
+        np.save(os.path.join(out_dir, "a.npy"), recv[0].numpy())
+        np.save(os.path.join(out_dir, "m.npy"), recv[1].numpy())
+    env.barrier()
+    torch.distributed.destroy_process_group()
+
+
+def test_chunked_gather_pieces(tmp_path):
+    world = 2
+    mp.spawn(_chunked_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    a = np.load(tmp_path / "a.npy")
+    m = np.load(tmp_path / "m.npy")
+    for r in range(world):
+        assert np.array_equal(a[r], np.arange(103) + 1000 * r)
+        assert np.array_equal(m[r], np.arange(103, dtype=np.float32) * 0.5 + r)
