@@ -194,6 +194,7 @@ struct PairArgs {
     int32_t n_cams, n_pairs, row_blocks;
     int32_t rows_per_wg;        // kWaves * RPW * row groups
     int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
+    int32_t lane_results;       // 1: one RPW-lane store per group; 0: one store per row
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -203,6 +204,25 @@ struct ColRegs {
     double x[kColsPerLane], y[kColsPerLane];
     uint32_t state[kColsPerLane];   // kOk / kDeg / kNone / kWild
 };
+
+// Row stores of the argmin / min of rows r0..r0+RPW-1: lane r holds row r's
+// result (one store instruction with RPW active lanes instead of RPW stores).
+template <int RPW>
+__device__ __forceinline__ void store_row_results(const uint32_t (&kmin)[RPW],
+                                                  const int32_t (&imin)[RPW], int nrows, int lane,
+                                                  int32_t *argmin, float *minval, int64_t row0) {
+    uint32_t k = kKeyInvalid;
+    int32_t ix = 0;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        k = (lane == r) ? kmin[r] : k;
+        ix = (lane == r) ? imin[r] : ix;
+    }
+    if (lane < nrows) {
+        if (argmin) argmin[row0 + lane] = (k == kKeyInvalid) ? -1 : ix;
+        if (minval) minval[row0 + lane] = value_of_key(k);
+    }
+}
 
 // 0.5 * s for s >= +0 finite, as bits, EXACT after the float32 cast: the
 // saturating decrement of the exponent field halves every s >= 2^-1021
@@ -447,17 +467,22 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
         }
 
         if (ARGMIN && args.row_offs && nrows > 0) {
-            const int64_t roff = args.row_offs[sp];
+            uint32_t kmin[RPW];
+            int32_t imin[RPW];
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                if (r < nrows) {
-                    uint32_t kmin;
-                    int32_t imin;
-                    wave_argmin(best_key(best[r]), best[r].j, kmin, imin);
-                    if (lane == 0) {
-                        if (args.argmin) args.argmin[roff + grow0 + r] = (kmin == kKeyInvalid) ? -1 : imin;
-                        if (args.minval) args.minval[roff + grow0 + r] = value_of_key(kmin);
-                    }
+            for (int r = 0; r < RPW; ++r) {   // independent DPP chains interleave
+                kmin[r] = kKeyInvalid;
+                imin[r] = 0;
+                if (r < nrows) wave_argmin(best_key(best[r]), best[r].j, kmin[r], imin[r]);
+            }
+            if (args.lane_results) {
+                store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                       args.row_offs[sp] + grow0);
+            } else if (lane == 0) {
+                for (int r = 0; r < nrows; ++r) {
+                    const int64_t row = args.row_offs[sp] + grow0 + r;
+                    if (args.argmin) args.argmin[row] = (kmin[r] == kKeyInvalid) ? -1 : imin[r];
+                    if (args.minval) args.minval[row] = value_of_key(kmin[r]);
                 }
             }
         }
@@ -624,6 +649,97 @@ struct Cube256Args {
     int32_t j_blocks, i_splits, i_chunk;
 };
 
+// Sweep i in [i_begin, i_end) for RPW rows j0.. of one scene.  FULL: P == 256
+// and the cube rows are 16-byte aligned, so every lane owns 4 valid k and all
+// loads/stores are unconditional vectors.
+template <int RPW, bool FULL>
+__device__ __forceinline__ void triplet_rows(const Cube256Args &args, const double *e12,
+                                             const double *e13, const double *e23, int M, int P,
+                                             int j0, int nrows, int i_begin, int i_end,
+                                             int64_t coff, int64_t roff, int lane) {
+    const int kb = kColsPerLane * lane;
+    const int kvalid = FULL ? kColsPerLane : P - kb;
+    double a23[RPW][kColsPerLane];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r)
+        load4(e23 + (int64_t)(j0 + min(r, nrows - 1)) * args.ld + kb, kvalid, a23[r]);
+
+    // software pipeline: e13 row and e12 slice of i+1 are loaded during row i
+    double n13[kColsPerLane], n12[RPW];
+    auto fetch = [&](int i) {
+        load4(e13 + (int64_t)i * args.ld + kb, kvalid, n13);
+#pragma unroll
+        for (int r = 0; r < RPW; r += 2) {
+            const f64x2 v2 = *reinterpret_cast<const f64x2 *>(e12 + (int64_t)i * args.ld + j0 + r);
+            n12[r] = v2.x;
+            n12[r + 1] = v2.y;
+        }
+    };
+    fetch(i_begin);
+    for (int i = i_begin; i < i_end; ++i) {
+        double a13[kColsPerLane], a12[RPW];
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) a13[q] = n13[q];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) a12[r] = n12[r];
+        if (i + 1 < i_end) fetch(i + 1);
+
+        uint32_t key[RPW];
+        int32_t idx[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            key[r] = kKeyInvalid;
+            idx[r] = 0x7FFFFFFF;
+            if (r >= nrows) continue;   // uniform
+            double sum[kColsPerLane], q0[kColsPerLane];
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                sum[q] = (a12[r] + a13[q]) + a23[r][q];       // (e12 + e13) + e23, :81
+                q0[q] = sum[q] * kThird;
+                ok &= third_fast_ok(q0[q]);
+            }
+            float v[kColsPerLane];
+            const int64_t row = (int64_t)i * M + j0 + r;
+            if (FULL && args.cube && __all(ok)) {   // finite, fast division exact
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                              (uint32_t)kb * 4u, v);
+                Best b{v[0], kb};
+#pragma unroll
+                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                key[r] = __float_as_uint(b.v) + 1u;
+                idx[r] = b.j;
+            } else {
+                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    v[q] = (float)qq;
+                    if (q < kvalid) {
+                        if (args.cube)
+                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                        best_update_safe(b, v[q], kb + q);
+                    }
+                }
+                key[r] = best_key(b);
+                idx[r] = b.j;
+            }
+        }
+        uint32_t kmin[RPW];
+        int32_t imin[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {   // independent DPP chains interleave
+            kmin[r] = kKeyInvalid;
+            imin[r] = 0;
+            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+        }
+        store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                               roff + (int64_t)i * M + j0);
+    }
+}
+
 template <int RPW>
 __global__ __launch_bounds__(kThreads) void triplet256_kernel(Cube256Args args) {
     const int t = threadIdx.x;
@@ -643,92 +759,15 @@ __global__ __launch_bounds__(kThreads) void triplet256_kernel(Cube256Args args) 
     const int i_end = min(N, i_begin + args.i_chunk);
     if (j0 >= M || i_begin >= N || P == 0) return;   // wave-uniform; no barriers below
     const int nrows = min(RPW, M - j0);
-
     const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
     const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride;
     const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
-    const int kb = kColsPerLane * lane;
-    bool kval[kColsPerLane];
-#pragma unroll
-    for (int q = 0; q < kColsPerLane; ++q) kval[q] = kb + q < P;
     const int64_t coff = args.cube_offs[s];
-    const bool fast_shape = (P == kChunk) && ((coff & 3) == 0) && args.cube;
-
-    const int kvalid = P - kb;   // valid columns of this lane (may be <= 0)
-    double a23[RPW][kColsPerLane];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r)
-        load4(e23 + (int64_t)(j0 + min(r, nrows - 1)) * args.ld + kb, kvalid, a23[r]);
-
     const int64_t roff = args.row_offs[s];
-    for (int i = i_begin; i < i_end; ++i) {
-        double a13[kColsPerLane];
-        load4(e13 + (int64_t)i * args.ld + kb, kvalid, a13);
-        // e12[i][j0 .. j0+RPW): the same 64 bytes for every lane (broadcast)
-        double a12[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; r += 2) {
-            const f64x2 v2 = *reinterpret_cast<const f64x2 *>(e12 + (int64_t)i * args.ld + j0 + r);
-            a12[r] = v2.x;
-            a12[r + 1] = v2.y;
-        }
-        uint32_t key[RPW];
-        int32_t idx[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            key[r] = kKeyInvalid;
-            idx[r] = 0x7FFFFFFF;
-            if (r >= nrows) continue;   // uniform
-            const double v12 = a12[r];
-            double sum[kColsPerLane], q0[kColsPerLane];
-            bool ok = true;
-#pragma unroll
-            for (int q = 0; q < kColsPerLane; ++q) {
-                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
-                q0[q] = sum[q] * kThird;
-                ok &= third_fast_ok(q0[q]);
-            }
-            float v[kColsPerLane];
-            const int64_t row = (int64_t)i * M + j0 + r;
-            if (fast_shape && __all(ok)) {   // every lane valid, finite, fast division exact
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                              (uint32_t)kb * 4u, v);
-                Best b{v[0], kb};
-#pragma unroll
-                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                key[r] = __float_as_uint(b.v) + 1u;
-                idx[r] = b.j;
-            } else {
-                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
-                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                    v[q] = (float)qq;
-                    if (kval[q]) {
-                        if (args.cube) __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
-                        best_update_safe(b, v[q], kb + q);
-                    }
-                }
-                key[r] = best_key(b);
-                idx[r] = b.j;
-            }
-        }
-        // batched per-row reductions (independent DPP chains interleave)
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            if (r >= nrows) continue;
-            uint32_t kmin;
-            int32_t imin;
-            wave_argmin(key[r], idx[r], kmin, imin);
-            if (lane == 0) {
-                const int64_t row = roff + (int64_t)i * M + j0 + r;
-                if (args.argmin) args.argmin[row] = (kmin == kKeyInvalid) ? -1 : imin;
-                if (args.minval) args.minval[row] = value_of_key(kmin);
-            }
-        }
-    }
+    if (P == kChunk && (coff & 3) == 0)
+        triplet_rows<RPW, true>(args, e12, e13, e23, M, P, j0, nrows, i_begin, i_end, coff, roff, lane);
+    else
+        triplet_rows<RPW, false>(args, e12, e13, e23, M, P, j0, nrows, i_begin, i_end, coff, roff, lane);
 }
 
 // ------------------------------------------------------- write probe ----
@@ -748,7 +787,7 @@ __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;       // pairwise default: 64 rows per workgroup
 constexpr int kTripletRowsPerWave = 8; // generic triplet: 32 (i, j) rows per workgroup
-constexpr int kTriplet256RowsPerWave = 8;   // P <= 256 triplet: e23 rows held per wave
+constexpr int kTriplet256RowsPerWave = 4;   // P <= 256 triplet: e23 rows held per wave
 
 thread_local char g_err[512];
 
@@ -787,6 +826,16 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
     return MVM_OK;
 }
 
+// Tuning knobs (read per launch; defaults tuned on MI355X):
+//   MVM_PAIRWISE_LANE_RESULTS  1: argmin rows stored by RPW lanes at once
+//   MVM_TRIPLET_RPW / MVM_TRIPLET_GENERIC  cube kernel variant
+//   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
+//   MVM_PAIRWISE_RG   row groups per wave (1..16)
+int env_int(const char *name, int dflt) {
+    const char *e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 
 template <int RPW>
@@ -799,6 +848,7 @@ template <int RPW>
 void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_cols,
                          int row_groups, bool argmin, bool f64, hipStream_t stream) {
     a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
+    a.lane_results = env_int("MVM_PAIRWISE_LANE_RESULTS", 1);
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
@@ -812,13 +862,6 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     }
 }
 
-// Tuning knobs (read per launch; defaults tuned on MI355X):
-//   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
-//   MVM_PAIRWISE_RG   row groups per wave (1..16)
-int env_int(const char *name, int dflt) {
-    const char *e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
 
 int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int32_t max_cols,
                            bool argmin, bool f64, hipStream_t stream) {
@@ -964,7 +1007,7 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     if (st) return st;
     if (max_n <= kChunk && env_int("MVM_TRIPLET_GENERIC", 0) == 0) {
         // every P <= 256: register-resident e23 kernel
-        constexpr int rpw = kTriplet256RowsPerWave;
+        const int rpw = env_int("MVM_TRIPLET_RPW", kTriplet256RowsPerWave) == 8 ? 8 : 4;
         Cube256Args c{};
         c.cam_offs = cam_offs_dev;
         c.e = (const double *)workspace_dev;
@@ -987,7 +1030,10 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
         if (blocks > 0x7FFFFFFFLL)
             return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                         (long long)blocks);
-        triplet256_kernel<rpw><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+        if (rpw == 4)
+            triplet256_kernel<4><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+        else
+            triplet256_kernel<8><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
         return check_launch("triplet256_kernel");
     }
     CubeArgs c{};

@@ -19,7 +19,7 @@ ap.add_argument("--scenes", type=int, default=1000)
 ap.add_argument("--cams", type=int, default=4)
 ap.add_argument("--dets", type=int, default=1024)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="4,8,16")
+ap.add_argument("--variants", default="4,8,16", help="RPW or RPW:RG list")
 ap.add_argument("--no-dist", action="store_true")
 args = ap.parse_args()
 
@@ -38,7 +38,14 @@ times = {v: [] for v in variants}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in variants:
-        os.environ["MVM_PAIRWISE_RPW"] = v
+        rpw, _, rg = v.partition(":")
+        rg, _, lr = rg.partition(":")
+        os.environ["MVM_PAIRWISE_LANE_RESULTS"] = lr or "1"
+        os.environ["MVM_PAIRWISE_RPW"] = rpw
+        if rg:
+            os.environ["MVM_PAIRWISE_RG"] = rg
+        else:
+            os.environ.pop("MVM_PAIRWISE_RG", None)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ops.pairwise_residual_argmin(pts, co, F, plan, out=(dist, am, mv))   # warm this variant
         e0.record()
@@ -54,6 +61,6 @@ for rnd in range(args.rounds + 1):
         assert chk == ref, f"variant {v} differs"
 for v in variants:
     t = np.array(times[v])
-    print(f"RPW={v:>3}: median {np.median(t):.3f} ms  min {t.min():.3f} ms  "
+    print(f"RPW:RG={v:>5}: median {np.median(t):.3f} ms  min {t.min():.3f} ms  "
           f"{nbytes / (np.median(t) * 1e-3) / 1e9:.0f} GB/s  "
           f"{plan.n_dist / (np.median(t) * 1e-3):.3e} pairs/s")
