@@ -96,3 +96,34 @@ def fundamental_matrices(Ks: Sequence[np.ndarray], RTs: Sequence[np.ndarray],
                                        Ks[b], RTs[b][:3, :3], RTs[b][:3, 3])
         out[p] = np.asarray(F, dtype=np.float64).reshape(9)
     return out
+
+
+def fundamental_matrices_batched(Ks: np.ndarray, RTs: np.ndarray, pairs: np.ndarray) -> np.ndarray:
+    """F for every (scene, pair) at once -> float64 [S*P, 9].
+
+    ``Ks`` float32 [S, C, 3, 3], ``RTs`` float64 [S, C, 4, 4].  Same operations,
+    dtypes and order as ``compute_fundamental_matrix`` (camera_utils.py:23-46),
+    vectorised over scenes and pairs with stacked matmuls; numpy evaluates a
+    stacked matmul matrix by matrix, so the bits equal the per-pair function
+    (tests/test_host_logic.py checks this on this host's BLAS).
+    """
+    Ks = np.asarray(Ks)
+    RTs = np.asarray(RTs, dtype=np.float64)
+    pairs = np.asarray(pairs, dtype=np.int64).reshape(-1, 2)
+    a, b = pairs[:, 0], pairs[:, 1]
+    RT1, RT2 = RTs[:, a], RTs[:, b]                            # [S, P, 4, 4]
+    R1, R2 = RT1[..., :3, :3], RT2[..., :3, :3]
+    t1, t2 = RT1[..., :3, 3], RT2[..., :3, 3]                  # [S, P, 3]
+    R_rel = R2 @ np.swapaxes(R1, -1, -2)
+    t_rel = t2 - (R_rel @ t1[..., None])[..., 0]
+    skew = np.zeros(R_rel.shape, dtype=np.float32)
+    skew[..., 0, 1], skew[..., 0, 2] = -t_rel[..., 2], t_rel[..., 1]
+    skew[..., 1, 0], skew[..., 1, 2] = t_rel[..., 2], -t_rel[..., 0]
+    skew[..., 2, 0], skew[..., 2, 1] = -t_rel[..., 1], t_rel[..., 0]
+    essential = skew @ R_rel
+    K1inv = np.linalg.inv(Ks[:, a])
+    K2inv = np.linalg.inv(Ks[:, b])
+    F = np.swapaxes(K2inv, -1, -2) @ essential @ K1inv
+    f22 = F[..., 2:3, 2:3]
+    F = np.where(np.abs(f22) > 1e-8, F / np.where(np.abs(f22) > 1e-8, f22, 1.0), F)
+    return np.ascontiguousarray(F.reshape(-1, 9), dtype=np.float64)

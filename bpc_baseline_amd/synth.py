@@ -25,7 +25,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
-from .inference.utils.camera_utils import calc_pose_matrix, camera_pairs, fundamental_matrices
+from .inference.utils.camera_utils import (calc_pose_matrix, camera_pairs,
+                                           fundamental_matrices_batched)
 
 __all__ = ["IPD_K", "SceneBatch", "make_rig", "make_capture", "make_scenes"]
 
@@ -153,19 +154,21 @@ def make_scenes(n_scenes: int, n_cams: int, n_dets, *, seed: int = 0, first_scen
         pairs = camera_pairs(n_cams)
     pts_parts: List[np.ndarray] = []
     counts = np.zeros((n_scenes, n_cams), dtype=np.int64)
-    F = np.empty((n_scenes, len(pairs), 9), dtype=np.float64)
+    K_all = np.empty((n_scenes, n_cams, 3, 3), dtype=np.float32)
+    RT_all = np.empty((n_scenes, n_cams, 4, 4), dtype=np.float64)
     for s in range(n_scenes):
         rng = np.random.default_rng(seed + first_scene + s)
         per_view = rng.integers(0, int(n_dets) + 1, size=n_cams) if ragged else [int(n_dets)] * n_cams
         Ks, RTs = make_rig(rng, n_cams)
-        F[s] = fundamental_matrices(Ks, RTs, pairs)
+        K_all[s], RT_all[s] = np.stack(Ks), np.stack(RTs)
         for c, (_, cxy) in enumerate(_views(rng, Ks, RTs, list(per_view), box_px=80.0, noise_px=1.5)):
             counts[s, c] = len(cxy)
             pts_parts.append(cxy)
+    F = fundamental_matrices_batched(K_all, RT_all, pairs) if n_scenes else np.zeros((0, 9))
     cam_offs = np.zeros(n_scenes * n_cams + 1, dtype=np.int64)
     np.cumsum(counts.reshape(-1), out=cam_offs[1:])
     pts = np.concatenate(pts_parts, axis=0) if pts_parts else np.zeros((0, 2))
     return SceneBatch(pts=np.ascontiguousarray(pts), cam_offs=cam_offs,
-                      F=np.ascontiguousarray(F.reshape(-1, 9)), pairs=np.asarray(pairs, np.int32),
+                      F=np.ascontiguousarray(F), pairs=np.asarray(pairs, np.int32),
                       n_scenes=n_scenes, n_cams=n_cams, seed=seed,
                       meta={"first_scene": first_scene, "n_dets": n_dets, "ragged": ragged})

@@ -161,3 +161,28 @@ def test_fast_division_by_three_rule():
         b = q0.astype(np.float32).view(np.int32)
     assert not np.any((a != b) & ok)
     assert ok[1_000_000:2_000_000].mean() > 0.999   # realistic costs take the fast path
+
+
+def test_batched_fundamental_matrices_bit_equal():
+    """§8f #2: batched F == the per-pair restatement of compute_fundamental_matrix,
+    bit for bit on this host (same numpy/BLAS kernels, matrix by matrix)."""
+    from bpc_baseline_amd.synth import make_rig
+    from bpc_baseline_amd.inference.utils.camera_utils import (
+        camera_pairs, fundamental_matrices, fundamental_matrices_batched)
+    rng = np.random.default_rng(3)
+    rigs = [make_rig(rng, 4) for _ in range(50)]
+    Ks = np.stack([np.stack(k) for k, _ in rigs])
+    RTs = np.stack([np.stack(r) for _, r in rigs])
+    pairs = camera_pairs(4)
+    ref = np.concatenate([fundamental_matrices(list(k), list(r), pairs) for k, r in zip(Ks, RTs)])
+    got = fundamental_matrices_batched(Ks, RTs, pairs)
+    assert np.array_equal(ref.view(np.int64), got.view(np.int64))
+
+
+def test_batched_fundamental_matrices_vs_reference(golden):
+    from bpc_baseline_amd.inference.utils.camera_utils import fundamental_matrices_batched
+    g = golden("a6_fundamental.npz")
+    RT = np.zeros((len(g["R"]), 2, 4, 4))
+    RT[..., :3, :3], RT[..., :3, 3], RT[..., 3, 3] = g["R"], g["t"], 1.0
+    got = fundamental_matrices_batched(g["K"], RT, np.array([[0, 1]]))
+    np.testing.assert_allclose(got.reshape(-1, 3, 3), g["F"], rtol=1e-12, atol=1e-18)

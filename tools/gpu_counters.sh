@@ -1,14 +1,12 @@
 set -o pipefail
-mkdir -p gpurun_out/ctr
+mkdir -p gpurun_out/ctr2
 export TMPDIR=/tmp
-rocprofv3 -L > gpurun_out/ctr/counters_list.txt 2>&1 || true
-grep -o "SQ_[A-Z0-9_]*\|GRBM_[A-Z0-9_]*\|TA_[A-Z0-9_]*BUSY[A-Z0-9_]*\|TCP_[A-Z0-9_]*" gpurun_out/ctr/counters_list.txt | sort -u > gpurun_out/ctr/names.txt || true
-export MVM_PAIRWISE_RPW=16
 P1="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU"
-P2="GRBM_GUI_ACTIVE GRBM_COUNT SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES SQ_ACTIVE_INST_LDS"
+P2="GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_SMEM SQ_WAVES SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_WR"
+P3="TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum"
 i=0
-for P in "$P1" "$P2"; do
+for P in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d gpurun_out/ctr/p$i -o run -- python tools/tune_pairwise.py --rounds 1 --variants 16 > gpurun_out/ctr/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/ctr/p$i.log; }
+  timeout -k 10 300 rocprofv3 --pmc $P --output-format csv -d gpurun_out/ctr2/p$i -o run -- python tools/tune_cube.py --rounds 1 --variants rpw4 > gpurun_out/ctr2/p$i.log 2>&1 || { echo "pass $i failed"; tail -5 gpurun_out/ctr2/p$i.log; }
 done
 echo done
