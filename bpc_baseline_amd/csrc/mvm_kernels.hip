@@ -770,6 +770,151 @@ __global__ __launch_bounds__(kThreads) void triplet256_kernel(Cube256Args args) 
         triplet_rows<RPW, false>(args, e12, e13, e23, M, P, j0, nrows, i_begin, i_end, coff, roff, lane);
 }
 
+// ------------------------------------------- tiled triplet kernel (v3) ----
+// Same arithmetic as triplet256_kernel, different schedule: a workgroup owns
+// (scene, 16 consecutive j, IB consecutive i).  Its prologue loads everything
+// the tile needs -- e23 rows into registers, the e13[i-block][:] and
+// e12[i-block][j-block] tiles into LDS -- with ONE wait; the main loop then
+// issues only LDS reads, VALU work and stores.  This matters on CDNA, where
+// vmcnt counts loads and stores together in issue order: a global load
+// issued after a row store waits for that store's acknowledgement, so loads
+// inside a store-streaming loop stall it.
+
+struct Cube3Args {
+    const int64_t *cam_offs;
+    const double *e;
+    int64_t mat_stride;
+    int64_t ld;
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t j_blocks, i_blocks;
+};
+
+template <int kCubeIB, int kCubeRPW>   // i rows per tile, j rows per wave
+__global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) {
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];              // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kWaves * kCubeRPW];   // 2 KiB
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blockIdx.x / per_scene);
+    const int rem = (int)(blockIdx.x % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t c0 = args.cam_offs[3 * (int64_t)s];
+    const int N = (int)(args.cam_offs[3 * (int64_t)s + 1] - c0);
+    const int M = (int)(args.cam_offs[3 * (int64_t)s + 2] - args.cam_offs[3 * (int64_t)s + 1]);
+    const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
+    const int jw0 = jb * kWaves * kCubeRPW;            // first j of the workgroup
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;              // this wave's first j
+    const int nrows = min(kCubeRPW, M - j0);           // may be <= 0 (scalar)
+
+    const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
+    const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride;
+    const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
+    const int kb = kColsPerLane * lane;
+    const int kvalid = P - kb;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    const bool full = (P == kChunk) && ((coff & 3) == 0) && args.cube;
+
+    // ---- prologue: all loads of the tile, then one barrier ----------------
+    double a23[kCubeRPW][kColsPerLane];
+#pragma unroll
+    for (int r = 0; r < kCubeRPW; ++r)
+        load4(e23 + (int64_t)(j0 + max(0, min(r, nrows - 1))) * args.ld + kb, kvalid, a23[r]);
+    for (int x = t; x < kCubeIB * (kChunk / 2); x += kThreads) {   // e13 tile, 16 B per load
+        const int r = x / (kChunk / 2), c = 2 * (x % (kChunk / 2));
+        f64x2 v = {0.0, 0.0};
+        if (r < ni && c < P) {
+            if (c + 1 < P) {
+                v = *reinterpret_cast<const f64x2 *>(e13 + (int64_t)(i0 + r) * args.ld + c);
+            } else {
+                v.x = e13[(int64_t)(i0 + r) * args.ld + c];
+            }
+        }
+        *reinterpret_cast<f64x2 *>(&s13[r][c]) = v;
+    }
+    for (int x = t; x < kCubeIB * kWaves * kCubeRPW; x += kThreads) {
+        const int r = x / (kWaves * kCubeRPW), c = x % (kWaves * kCubeRPW);
+        s12[r][c] = (r < ni && jw0 + c < M) ? e12[(int64_t)(i0 + r) * args.ld + jw0 + c] : 0.0;
+    }
+    __syncthreads();
+    if (nrows <= 0) return;   // after the barrier: no more barriers below
+
+    for (int ii = 0; ii < ni; ++ii) {
+        const int i = i0 + ii;
+        double a13[kColsPerLane];
+        {
+            const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+            const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+            a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+        }
+        uint32_t key[kCubeRPW];
+        int32_t idx[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            key[r] = kKeyInvalid;
+            idx[r] = 0x7FFFFFFF;
+            if (r >= nrows) continue;   // uniform
+            const double v12 = s12[ii][wave * kCubeRPW + r];
+            double sum[kColsPerLane], q0[kColsPerLane];
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                q0[q] = sum[q] * kThird;
+                ok &= third_fast_ok(q0[q]);
+            }
+            float v[kColsPerLane];
+            const int64_t row = (int64_t)i * M + j0 + r;
+            if (full && __all(ok)) {
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                              (uint32_t)kb * 4u, v);
+                Best b{v[0], kb};
+#pragma unroll
+                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                key[r] = __float_as_uint(b.v) + 1u;
+                idx[r] = b.j;
+            } else {
+                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    v[q] = (float)qq;
+                    if (q < kvalid) {
+                        if (args.cube)
+                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                        best_update_safe(b, v[q], kb + q);
+                    }
+                }
+                key[r] = best_key(b);
+                idx[r] = b.j;
+            }
+        }
+        uint32_t kmin[kCubeRPW];
+        int32_t imin[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            kmin[r] = kKeyInvalid;
+            imin[r] = 0;
+            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+        }
+        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                    roff + (int64_t)i * M + j0);
+    }
+}
+
 // ------------------------------------------------------- write probe ----
 // Speed-of-light reference for the roofline: every workgroup writes one
 // contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
@@ -1005,7 +1150,39 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     int st = mvm_pairwise_residual_f64(pts_dev, cam_offs_dev, F_dev, pa, pb, n_scenes, 3, 3,
                                        max_n, mat_stride, ld, (double *)workspace_dev, stream);
     if (st) return st;
-    if (max_n <= kChunk && env_int("MVM_TRIPLET_GENERIC", 0) == 0) {
+    const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled, 2 register, 1 generic
+    if (max_n <= kChunk && variant == 3) {
+        // tile shape knob MVM_TRIPLET_TILE: 3 = 16i x 32j (default, fastest on
+        // MI355X), 0 = 16i x 16j, 1 = 8i x 16j, 2 = 8i x 32j
+        const int tile = env_int("MVM_TRIPLET_TILE", 3);
+        const int ib = (tile == 1 || tile == 2) ? 8 : 16;
+        const int rpw = (tile == 2 || tile == 3) ? 8 : 4;
+        Cube3Args c{};
+        c.cam_offs = cam_offs_dev;
+        c.e = (const double *)workspace_dev;
+        c.mat_stride = mat_stride;
+        c.ld = ld;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.j_blocks = (max_n + kWaves * rpw - 1) / (kWaves * rpw);
+        c.i_blocks = (max_n + ib - 1) / ib;
+        const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
+        if (blocks > 0x7FFFFFFFLL)
+            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+        const dim3 grid((unsigned)blocks), block(kThreads);
+        switch (tile) {
+        case 1: triplet_tile_kernel<8, 4><<<grid, block, 0, s>>>(c); break;
+        case 2: triplet_tile_kernel<8, 8><<<grid, block, 0, s>>>(c); break;
+        case 0: triplet_tile_kernel<16, 4><<<grid, block, 0, s>>>(c); break;
+        default: triplet_tile_kernel<16, 8><<<grid, block, 0, s>>>(c); break;
+        }
+        return check_launch("triplet_tile_kernel");
+    }
+    if (max_n <= kChunk && variant == 2) {
         // every P <= 256: register-resident e23 kernel
         const int rpw = env_int("MVM_TRIPLET_RPW", kTriplet256RowsPerWave) == 8 ? 8 : 4;
         Cube256Args c{};

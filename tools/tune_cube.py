@@ -8,7 +8,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=250)
 ap.add_argument("--dets", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="rpw8,rpw4,generic")
+ap.add_argument("--variants", default="tile,rpw4,generic")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 b = make_scenes(args.scenes, 3, args.dets, seed=0)
@@ -18,13 +18,19 @@ out = (torch.empty(plan.n_cube, dtype=torch.float32, device=dev),
        torch.empty(plan.n_rows, dtype=torch.int32, device=dev),
        torch.empty(plan.n_rows, dtype=torch.float32, device=dev))
 nbytes = 4.0 * plan.n_cube + 8.0 * plan.n_rows + 16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0]
-env = {"rpw8": {"MVM_TRIPLET_RPW": "8"}, "rpw4": {"MVM_TRIPLET_RPW": "4"},
-       "generic": {"MVM_TRIPLET_GENERIC": "1"}}
+env = {"tile": {"MVM_TRIPLET_VARIANT": "3"},
+       "t16x16": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "0"},
+       "t8x16": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "1"},
+       "t8x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "2"},
+       "t16x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "3"},
+       "rpw8": {"MVM_TRIPLET_VARIANT": "2", "MVM_TRIPLET_RPW": "8"},
+       "rpw4": {"MVM_TRIPLET_VARIANT": "2", "MVM_TRIPLET_RPW": "4"},
+       "generic": {"MVM_TRIPLET_VARIANT": "1"}}
 times = {v: [] for v in args.variants.split(",")}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in times:
-        for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_GENERIC"):
+        for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_VARIANT", "MVM_TRIPLET_TILE"):
             os.environ.pop(k, None)
         os.environ.update(env[v])
         ops.triplet_cost_argmin(pts, co, F, plan, out=out)
