@@ -325,7 +325,8 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     double *s_x = s_l2 + T;
     double *s_y = s_x + T;
     double(*s_row)[RPW][6] = reinterpret_cast<double(*)[RPW][6]>(s_y + T);   // per wave
-    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_y + T + kWaves * RPW * 6);
+    double *s_rpt = s_y + T + kWaves * RPW * 6;              // row centroids of the workgroup
+    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
 
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
@@ -370,11 +371,17 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
             s_cst[jj] = st;
         }
     };
-    const int n_tiles = (nb + T - 1) / T;
-    if (n_tiles == 1) {
-        load_tile(0);
-        __syncthreads();
+    // every global load of the workgroup's rows happens here, before the first
+    // store (on CDNA vmcnt orders loads behind earlier stores)
+    for (int x = t; x < args.rows_per_wg; x += kThreads) {
+        const int i = row0 + x;
+        const f64x2 v = (i < na) ? *reinterpret_cast<const f64x2 *>(args.pts + 2 * (oa + i))
+                                 : f64x2{0.0, 0.0};
+        *reinterpret_cast<f64x2 *>(s_rpt + 2 * x) = v;
     }
+    const int n_tiles = (nb + T - 1) / T;
+    if (n_tiles == 1) load_tile(0);
+    __syncthreads();
 
     const int wg_rows = min(args.rows_per_wg, na - row0);
     const int n_groups = (wg_rows + kWaves * RPW - 1) / (kWaves * RPW);   // uniform over the WG
@@ -386,8 +393,8 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
             double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
             bool deg = true;
             if (lane < nrows) {
-                x = args.pts[2 * (oa + i)];
-                y = args.pts[2 * (oa + i) + 1];
+                x = s_rpt[2 * (i - row0)];
+                y = s_rpt[2 * (i - row0) + 1];
                 deg = row_line(f, x, y, l0, l1, l2);
             }
             s_row[wave][lane][0] = l0;
@@ -984,9 +991,9 @@ int env_int(const char *name, int dflt) {
 constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 
 template <int RPW>
-size_t pairwise_lds_bytes(int col_tile) {
+size_t pairwise_lds_bytes(int col_tile, int rows_per_wg) {
     return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
-           (size_t)kWaves * RPW * 6 * sizeof(double);
+           (size_t)kWaves * RPW * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double);
 }
 
 template <int RPW>
@@ -997,7 +1004,7 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
-    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile);
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg);
     if (f64) {
         pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
     } else if (argmin) {
