@@ -54,6 +54,10 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
         _vp, _vp, _vp, _vp, _vp,            # cube_offs, row_offs, cube, argmin, minval
         _vp, _sz, _vp]),                    # workspace, workspace_bytes, stream
+    "mvm_lsap_plan": (_i64, [_i32, _vp, _vp, _vp, _vp]),
+    "mvm_lsap_solve": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _vp, _vp,      # cost, cost_offs, dims, n, ws_offs, out_offs
+        _vp, _sz, _vp, _vp, _vp, _vp]),     # workspace, bytes, row_ind, col_ind, status, stream
     "mvm_hbm_write_probe": (ctypes.c_int, [_vp, _sz, _vp]),
 }
 

@@ -34,6 +34,7 @@
 #include <string.h>
 
 #include "mvmatch.h"
+#include "mvm_internal.h"
 
 #pragma clang fp contract(off)
 
@@ -941,22 +942,10 @@ constexpr int kRowsPerWave = 16;       // pairwise default: 64 rows per workgrou
 constexpr int kTripletRowsPerWave = 8; // generic triplet: 32 (i, j) rows per workgroup
 constexpr int kTriplet256RowsPerWave = 4;   // P <= 256 triplet: e23 rows held per wave
 
-thread_local char g_err[512];
-
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
-int fail(int code, const char *fmt, ...) {
-    va_list ap;
-    va_start(ap, fmt);
-    vsnprintf(g_err, sizeof g_err, fmt, ap);
-    va_end(ap);
-    return code;
-}
+int fail(int code, const char *fmt, ...);
 
-int check_launch(const char *what) {
-    const hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return fail(MVM_ERR_HIP, "%s: %s", what, hipGetErrorString(err));
-    return MVM_OK;
-}
+int check_launch(const char *what) { return mvm_check_launch(what); }
 
 int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
                int n_cams) {
@@ -1044,6 +1033,43 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
 
 }  // namespace
 
+// ============================================================ internals ====
+namespace {
+thread_local char g_err[512];
+}
+
+void mvm_set_error(const char *msg) {
+    snprintf(g_err, sizeof g_err, "%s", msg);
+}
+
+void mvm_clear_error() { mvm_clear_error(); }
+
+int mvm_fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+int mvm_check_launch(const char *what) {
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return mvm_fail(MVM_ERR_HIP, "%s: %s", what, hipGetErrorString(err));
+    return MVM_OK;
+}
+
+namespace {
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    char buf[512];
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    mvm_set_error(buf);
+    return code;
+}
+}  // namespace
+
 // ================================================================ C ABI ====
 extern "C" {
 
@@ -1068,7 +1094,7 @@ int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_
                                  int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
                                  const int64_t *row_offs_dev, float *dist_dev,
                                  int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream) {
-    g_err[0] = 0;
+    mvm_clear_error();
     PairArgs a{};
     int st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
     if (st) return st;
@@ -1096,7 +1122,7 @@ int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev
                               int32_t n_scenes, int32_t n_cams, int32_t n_pairs,
                               int32_t max_n, int64_t mat_stride, int64_t ld, double *e_dev,
                               mvm_stream_t stream) {
-    g_err[0] = 0;
+    mvm_clear_error();
     PairArgs a{};
     int st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
     if (st) return st;
@@ -1115,7 +1141,7 @@ int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev
 }
 
 int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
-    g_err[0] = 0;
+    mvm_clear_error();
     if (!dst_dev || (((uintptr_t)dst_dev) & 15) || (bytes & 15))
         return fail(MVM_ERR_INVALID_ARGUMENT, "write probe needs a 16-byte aligned buffer/size");
     const size_t n16 = bytes / 16;
@@ -1138,7 +1164,7 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                             const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                             float *cube_dev, int32_t *argmin_dev, float *minval_dev,
                             void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream) {
-    g_err[0] = 0;
+    mvm_clear_error();
     if (n_scenes < 0 || max_n < 0) return fail(MVM_ERR_INVALID_ARGUMENT, "negative sizes");
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
     if (!pts_dev || !cam_offs_dev || !F_dev || !row_offs_dev)

@@ -1,0 +1,356 @@
+// mvm_lsap.hip — batched rectangular linear-sum assignment on MI355X.
+//
+// Replaces the reference's association step: match_objects
+// (bpc/inference/epipolar_matching.py:100-116) calls
+// scipy.optimize.linear_sum_assignment on the (N*M, P) flattened cost cube.
+// scipy (pinned 1.14.0) implements Crouse's shortest-augmenting-path
+// algorithm; this kernel reproduces it decision for decision (oracle/lsap.py
+// restates it and is pinned to scipy and to the reference's golden matches):
+//   * a tall matrix is transposed (rows = the short side);
+//   * per short-side row, one Dijkstra-like search over the remaining
+//     columns, whose scan order is an array initialised in REVERSE column
+//     order and shrunk by swap-with-last removal;
+//   * per step: r = ((minVal + C[i][j]) - u[i]) - v[j] in fp64 (no FMA),
+//     spc[j] = min(spc[j], r); among the columns with the smallest spc the
+//     scan keeps the first one in scan order unless a later equal one is
+//     unassigned (then the LAST such one);
+//   * dual updates u[SR] += minVal - spc[col4row[.]], v[SC] -= minVal - spc[.].
+//
+// MI355X mapping: one 1024-thread workgroup per problem (scene).  The tall
+// cost is transposed once through LDS tiles into the workspace; per-column
+// state (spc, v f64; row4col, path, scan position i32) lives in the
+// workspace, indexed by column so every scan is a coalesced stream, and the
+// scan position array turns the sequential tie rule into an order-free
+// reduction: winner = max scan position among the unassigned minima if any,
+// else the min scan position among the minima.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+
+#include "mvmatch.h"
+#include "mvm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kLsapThreads = 1024;
+constexpr int kLsapWaves = kLsapThreads / 64;
+constexpr int kTile = 64;   // transpose tile
+
+struct LsapArgs {
+    const float *cost;
+    const int64_t *cost_offs;   // element offset of each problem's matrix
+    const int64_t *dims;        // [n][2]: rows, cols (row-major, ld = cols)
+    const int64_t *ws_offs;     // byte offset of each problem's workspace
+    unsigned char *ws;
+    const int64_t *out_offs;    // offset of each problem's min(rows, cols) output pairs
+    int64_t *row_ind;
+    int64_t *col_ind;
+    int32_t *status;            // 0 ok, 1 invalid entries (NaN / -inf), 2 infeasible
+};
+
+struct Red {
+    double m;      // smallest shortest-path cost seen
+    int32_t first; // smallest scan position holding m
+    int32_t last_free;   // largest scan position holding m with an unassigned column (-1: none)
+};
+
+__device__ __forceinline__ Red red_combine(Red a, Red b) {
+    if (b.m < a.m) return b;
+    if (a.m < b.m) return a;
+    a.first = min(a.first, b.first);
+    a.last_free = max(a.last_free, b.last_free);
+    return a;
+}
+
+__device__ __forceinline__ Red red_wave(Red r) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        Red o;
+        o.m = __shfl_xor(r.m, off, 64);
+        o.first = __shfl_xor(r.first, off, 64);
+        o.last_free = __shfl_xor(r.last_free, off, 64);
+        r = red_combine(r, o);
+    }
+    return r;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Layout {
+    size_t ct, spc, v, path, row4col, pos, rem, u, col4row, sr, sc, total;
+};
+
+__host__ __device__ inline Layout lsap_layout(int64_t nr, int64_t nc, bool transpose) {
+    Layout L;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += (bytes + 255) & ~(size_t)255;
+        return at;
+    };
+    L.ct = take(transpose ? (size_t)nr * nc * sizeof(float) : 0);
+    L.spc = take(nc * sizeof(double));
+    L.v = take(nc * sizeof(double));
+    L.path = take(nc * sizeof(int32_t));
+    L.row4col = take(nc * sizeof(int32_t));
+    L.pos = take(nc * sizeof(int32_t));
+    L.rem = take(nc * sizeof(int32_t));
+    L.u = take(nr * sizeof(double));
+    L.col4row = take(nr * sizeof(int32_t));
+    L.sr = take((nr + 1) * sizeof(int32_t));
+    L.sc = take((nr + 1) * sizeof(int32_t));
+    L.total = o;
+    return L;
+}
+
+__global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
+    __shared__ float s_tile[kTile][kTile + 1];
+    __shared__ Red s_red[kLsapWaves];
+    __shared__ int s_flag;
+    __shared__ int s_i, s_sink, s_nrem, s_nsr, s_nsc;
+    __shared__ double s_min;
+
+    const int t = threadIdx.x;
+    const int lane = t % 64, wave = t / 64;
+    const int p = blockIdx.x;
+    const int64_t R = a.dims[2 * p], K = a.dims[2 * p + 1];
+    if (R == 0 || K == 0) {
+        if (t == 0) a.status[p] = 0;
+        return;
+    }
+    const bool transpose = K < R;
+    const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
+    const Layout L = lsap_layout(nr, nc, transpose);
+    unsigned char *w = a.ws + a.ws_offs[p];
+    const float *C0 = a.cost + a.cost_offs[p];
+    double *spc = reinterpret_cast<double *>(w + L.spc);
+    double *v = reinterpret_cast<double *>(w + L.v);
+    int32_t *path = reinterpret_cast<int32_t *>(w + L.path);
+    int32_t *row4col = reinterpret_cast<int32_t *>(w + L.row4col);
+    int32_t *pos = reinterpret_cast<int32_t *>(w + L.pos);
+    int32_t *rem = reinterpret_cast<int32_t *>(w + L.rem);
+    double *u = reinterpret_cast<double *>(w + L.u);
+    int32_t *col4row = reinterpret_cast<int32_t *>(w + L.col4row);
+    int32_t *sr = reinterpret_cast<int32_t *>(w + L.sr);
+    int32_t *sc = reinterpret_cast<int32_t *>(w + L.sc);
+    const float *Ct = transpose ? reinterpret_cast<const float *>(w + L.ct) : C0;
+
+    // ---- validate (NaN / -inf, as scipy) and transpose a tall matrix -------
+    if (t == 0) s_flag = 0;
+    __syncthreads();
+    int bad = 0;
+    if (transpose) {
+        float *Ctw = reinterpret_cast<float *>(w + L.ct);   // [nr][nc] = C0^T
+        for (int64_t r0 = 0; r0 < R; r0 += kTile) {
+            for (int64_t c0 = 0; c0 < K; c0 += kTile) {
+                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                    const int rr = x / kTile, cc = x % kTile;
+                    float val = 0.f;
+                    if (r0 + rr < R && c0 + cc < K) {
+                        val = C0[(r0 + rr) * K + c0 + cc];
+                        bad |= (val != val) || (val == -INFINITY);
+                    }
+                    s_tile[rr][cc] = val;
+                }
+                __syncthreads();
+                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                    const int cc = x / kTile, rr = x % kTile;
+                    if (r0 + rr < R && c0 + cc < K) Ctw[(c0 + cc) * nc + r0 + rr] = s_tile[rr][cc];
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        for (int64_t x = t; x < R * K; x += kLsapThreads) {
+            const float val = C0[x];
+            bad |= (val != val) || (val == -INFINITY);
+        }
+    }
+    if (bad) atomicOr(&s_flag, 1);
+    for (int64_t j = t; j < nc; j += kLsapThreads) {
+        v[j] = 0.0;
+        row4col[j] = -1;
+        path[j] = -1;
+    }
+    for (int64_t i = t; i < nr; i += kLsapThreads) {
+        u[i] = 0.0;
+        col4row[i] = -1;
+    }
+    __syncthreads();
+    if (s_flag) {
+        if (t == 0) a.status[p] = 1;
+        return;
+    }
+
+    // ---- one shortest augmenting path per short-side row --------------------
+    for (int cur = 0; cur < nr; ++cur) {
+        for (int64_t j = t; j < nc; j += kLsapThreads) {
+            spc[j] = INFINITY;
+            pos[j] = (int32_t)(nc - 1 - j);   // scan array starts in reverse column order
+            rem[nc - 1 - j] = (int32_t)j;
+        }
+        if (t == 0) {
+            s_i = cur;
+            s_sink = -1;
+            s_nrem = (int)nc;
+            s_nsr = 0;
+            s_nsc = 0;
+            s_min = 0.0;
+        }
+        __syncthreads();
+        while (true) {
+            const int i = s_i;
+            const double min_val = s_min;
+            const double ui = u[i];
+            const float *Ci = Ct + (int64_t)i * nc;
+            Red best{INFINITY, 0x7FFFFFFF, -1};
+            for (int64_t j = t; j < nc; j += kLsapThreads) {
+                const int32_t pj = pos[j];
+                if (pj < 0) continue;   // already visited (removed from the scan)
+                const double r = ((min_val + (double)Ci[j]) - ui) - v[j];
+                double sj = spc[j];
+                if (r < sj) {
+                    path[j] = i;
+                    spc[j] = r;
+                    sj = r;
+                }
+                const bool free_col = row4col[j] == -1;
+                if (sj < best.m) {
+                    best.m = sj;
+                    best.first = pj;
+                    best.last_free = free_col ? pj : -1;
+                } else if (sj == best.m) {
+                    best.first = min(best.first, pj);
+                    if (free_col) best.last_free = max(best.last_free, pj);
+                }
+            }
+            best = red_wave(best);
+            if (lane == 0) s_red[wave] = best;
+            __syncthreads();
+            if (t == 0) {
+                Red r = s_red[0];
+                for (int k = 1; k < kLsapWaves; ++k) r = red_combine(r, s_red[k]);
+                sr[s_nsr++] = i;
+                if (r.m == INFINITY) {
+                    s_flag = 2;   // infeasible (scipy: "cost matrix is infeasible")
+                } else {
+                    const int index = r.last_free >= 0 ? r.last_free : r.first;
+                    const int j = rem[index];
+                    s_min = r.m;
+                    if (row4col[j] == -1) {
+                        s_sink = j;
+                    } else {
+                        s_i = row4col[j];
+                    }
+                    sc[s_nsc++] = j;
+                    const int last = rem[--s_nrem];
+                    rem[index] = last;
+                    pos[last] = index;
+                    pos[j] = -1;
+                }
+            }
+            __syncthreads();
+            if (s_flag || s_sink >= 0) break;
+        }
+        if (s_flag) {
+            if (t == 0) a.status[p] = 2;
+            return;
+        }
+        // dual updates (each entry independent: order-free)
+        const double min_val = s_min;
+        for (int k = t; k < s_nsr; k += kLsapThreads) {
+            const int i = sr[k];
+            if (i != cur) u[i] += min_val - spc[col4row[i]];
+        }
+        for (int k = t; k < s_nsc; k += kLsapThreads) {
+            const int j = sc[k];
+            v[j] -= min_val - spc[j];
+        }
+        __syncthreads();
+        if (t == 0) {
+            u[cur] += min_val;
+            int j = s_sink;
+            while (true) {   // augment along the path
+                const int i = path[j];
+                row4col[j] = i;
+                const int prev = col4row[i];
+                col4row[i] = j;
+                j = prev;
+                if (i == cur) break;
+            }
+        }
+        __syncthreads();
+    }
+
+    // ---- output pairs in scipy's order ------------------------------------
+    const int64_t o = a.out_offs[p];
+    if (transpose) {
+        // (col4row[k], k) sorted by col4row[k] (distinct): rank by counting
+        for (int64_t k = t; k < nr; k += kLsapThreads) {
+            const int32_t rk = col4row[k];
+            int64_t rank = 0;
+            for (int64_t k2 = 0; k2 < nr; ++k2) rank += col4row[k2] < rk;
+            a.row_ind[o + rank] = rk;
+            a.col_ind[o + rank] = k;
+        }
+    } else {
+        for (int64_t i = t; i < nr; i += kLsapThreads) {
+            a.row_ind[o + i] = i;
+            a.col_ind[o + i] = col4row[i];
+        }
+    }
+    if (t == 0) a.status[p] = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t mvm_lsap_plan(int32_t n_problems, const int64_t *rows, const int64_t *cols,
+                      int64_t *ws_offs, int64_t *out_offs) {
+    if (n_problems < 0 || (n_problems > 0 && (!rows || !cols || !ws_offs || !out_offs))) {
+        mvm_set_error("mvm_lsap_plan: invalid arguments");
+        return -1;
+    }
+    int64_t w = 0, o = 0;
+    for (int32_t p = 0; p < n_problems; ++p) {
+        if (rows[p] < 0 || cols[p] < 0 || rows[p] > 0x7FFFFFFF || cols[p] > 0x7FFFFFFF) {
+            mvm_set_error("mvm_lsap_plan: problem dimensions out of range");
+            return -1;
+        }
+        ws_offs[p] = w;
+        out_offs[p] = o;
+        const bool tr = cols[p] < rows[p];
+        const int64_t nr = tr ? cols[p] : rows[p], nc = tr ? rows[p] : cols[p];
+        w += (rows[p] && cols[p]) ? (int64_t)lsap_layout(nr, nc, tr).total : 0;
+        o += rows[p] < cols[p] ? rows[p] : cols[p];
+    }
+    ws_offs[n_problems] = w;
+    out_offs[n_problems] = o;
+    return w;
+}
+
+int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const int64_t *dims_dev,
+                   int32_t n_problems, const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
+                   void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
+                   int64_t *col_ind_dev, int32_t *status_dev, mvm_stream_t stream) {
+    mvm_clear_error();
+    if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
+    if (n_problems == 0) return MVM_OK;
+    if (!cost_dev || !cost_offs_dev || !dims_dev || !ws_offs_dev || !out_offs_dev ||
+        !row_ind_dev || !col_ind_dev || !status_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (!workspace_dev && workspace_bytes)
+        return mvm_fail(MVM_ERR_WORKSPACE, "null workspace");
+    LsapArgs a{cost_dev, cost_offs_dev, dims_dev, ws_offs_dev,
+               reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
+               col_ind_dev, status_dev};
+    lsap_kernel<<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0,
+                  reinterpret_cast<hipStream_t>(stream)>>>(a);
+    return mvm_check_launch("lsap_kernel");
+}
+
+}  // extern "C"

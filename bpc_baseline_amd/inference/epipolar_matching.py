@@ -11,10 +11,10 @@ reference's numpy evaluation:
   match_objects         (epipolar_matching.py:100-116)-> list[(i, j, k)]
   triangulate_multi_view(epipolar_matching.py:118-127)-> np.ndarray (3,)
 
-``match_objects`` keeps the reference's host-side Hungarian assignment
-(scipy ``linear_sum_assignment``) and ``triangulate_multi_view`` its
-6x4 SVD: both are O(1)-per-match host steps outside the GPU hot path
-(SURVEY §8f ranks them next).  The ``img*`` arguments only drove the
+``match_objects`` runs the assignment on the GPU (``mvm_lsap_solve``): the
+same shortest-augmenting-path algorithm as scipy's ``linear_sum_assignment``,
+with the same tie-breaking and output order.
+``triangulate_multi_view`` keeps the reference's 6x4 SVD on the host.  The ``img*`` arguments only drove the
 reference's matplotlib visualisation (:31-69, unreachable from
 compute_cost_matrix); they are accepted and ignored.
 
@@ -27,8 +27,6 @@ from typing import List, Sequence, Tuple
 
 import numpy as np
 import torch
-from scipy.optimize import linear_sum_assignment
-
 from .. import ops
 
 __all__ = [
@@ -136,11 +134,32 @@ def compute_cost_matrix(dets1, dets2, dets3, F12, F13, F23, img1=None, img2=None
     return cubes[0]
 
 
+_LSAP_ERRORS = {1: "matrix contains invalid numeric entries", 2: "cost matrix is infeasible"}
+
+
+def linear_sum_assignment(cost_matrix):
+    """GPU ``scipy.optimize.linear_sum_assignment`` for one matrix -> (row_ind, col_ind)."""
+    dev = _device()
+    cost = np.ascontiguousarray(np.asarray(cost_matrix, dtype=np.float32))
+    if cost.ndim != 2:
+        raise ValueError("expected a matrix")
+    plan = ops.LsapPlan([cost.shape[0]], [cost.shape[1]], device=dev)
+    cost_d = torch.from_numpy(cost.reshape(-1) if cost.size else np.zeros(1, np.float32)).to(dev)
+    offs = torch.zeros(1, dtype=torch.int64, device=dev)
+    r, c, st = ops.linear_sum_assignment_batched(cost_d, offs, plan)
+    status = int(st.cpu()[0])
+    if status:
+        raise ValueError(_LSAP_ERRORS.get(status, f"assignment failed ({status})"))
+    return r.cpu().numpy(), c.cpu().numpy()
+
+
 def match_objects(cost_matrix, threshold) -> List[Tuple[int, int, int]]:
     """Flatten -> Hungarian -> keep matches < threshold (epipolar_matching.py:100-116).
 
-    Host-side, as in the reference: scipy ``linear_sum_assignment`` on the
-    ``(N*M, P)`` flattening, strict ``<`` threshold, ``i = r // M``, ``j = r % M``.
+    The assignment runs on the GPU and equals scipy ``linear_sum_assignment``
+    on the ``(N*M, P)`` flattening; strict ``<`` threshold; ``i = r // M``,
+    ``j = r % M``.  Non-float32 cubes are assigned in float32, the dtype
+    compute_cost_matrix returns.
     """
     N, M, P = cost_matrix.shape
     flat = cost_matrix.reshape(N * M, P)
@@ -148,7 +167,7 @@ def match_objects(cost_matrix, threshold) -> List[Tuple[int, int, int]]:
     out = []
     for r, c in zip(rows, cols):
         if flat[r, c] < threshold:
-            out.append((r // M, r % M, c))
+            out.append((np.int64(r) // M, np.int64(r) % M, np.int64(c)))
     return out
 
 

@@ -27,7 +27,7 @@ from . import _native
 __all__ = [
     "PairwisePlan", "TripletPlan",
     "pairwise_residual_argmin", "pairwise_residual_f64", "triplet_cost_argmin",
-    "hbm_write_probe",
+    "hbm_write_probe", "LsapPlan", "linear_sum_assignment_batched",
 ]
 
 
@@ -133,6 +133,32 @@ def triplet_cost_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: 
 
 @triplet_cost_argmin_out.register_fake
 def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minval, workspace):
+    return None
+
+
+@torch.library.custom_op("mvmatch::lsap_solve_out",
+                         mutates_args=("workspace", "row_ind", "col_ind", "status"))
+def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
+                   out_offs: Tensor, workspace: Tensor, row_ind: Tensor, col_ind: Tensor,
+                   status: Tensor) -> None:
+    dev = cost.device
+    if dev.type != "cuda":
+        raise ValueError("cost must be a GPU tensor (the matcher has no CPU path)")
+    for t, n, dt in ((cost, "cost", torch.float32), (cost_offs, "cost_offs", torch.int64),
+                     (dims, "dims", torch.int64), (ws_offs, "ws_offs", torch.int64),
+                     (out_offs, "out_offs", torch.int64), (workspace, "workspace", torch.uint8),
+                     (row_ind, "row_ind", torch.int64), (col_ind, "col_ind", torch.int64),
+                     (status, "status", torch.int32)):
+        _require(t, n, dt, dev)
+    n = status.numel()
+    st = _native.load().mvm_lsap_solve(_p(cost), _p(cost_offs), _p(dims), n, _p(ws_offs),
+                                       _p(out_offs), _p(workspace), workspace.numel(),
+                                       _p(row_ind), _p(col_ind), _p(status), _stream(cost))
+    _native.check("mvm_lsap_solve", st)
+
+
+@lsap_solve_out.register_fake
+def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status):
     return None
 
 
@@ -257,3 +283,39 @@ def hbm_write_probe(buf: Tensor) -> None:
     nbytes = buf.numel() * buf.element_size() // 16 * 16
     st = _native.load().mvm_hbm_write_probe(_p(buf), nbytes, _stream(buf))
     _native.check("mvm_hbm_write_probe", st)
+
+
+class LsapPlan:
+    """Workspace / output layout of a batch of assignment problems (host dims)."""
+
+    def __init__(self, rows, cols, device: torch.device | str = "cuda"):
+        rows = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1)
+        cols = np.ascontiguousarray(cols, dtype=np.int64).reshape(-1)
+        n = rows.size
+        ws_offs = np.zeros(n + 1, np.int64)
+        out_offs = np.zeros(n + 1, np.int64)
+        total = _native.load().mvm_lsap_plan(n, rows.ctypes.data, cols.ctypes.data,
+                                             ws_offs.ctypes.data, out_offs.ctypes.data)
+        if total < 0:
+            raise _native.MvmError("mvm_lsap_plan", -1, _native.load().mvm_last_error_string().decode())
+        self.n = n
+        self.rows, self.cols = rows, cols
+        self.out_offs_host = out_offs
+        self.device = torch.device(device)
+        self.dims = torch.from_numpy(np.stack([rows, cols], axis=1).reshape(-1).copy()).to(self.device)
+        self.ws_offs = torch.from_numpy(ws_offs).to(self.device)
+        self.out_offs = torch.from_numpy(out_offs).to(self.device)
+        self.workspace = torch.empty(max(int(total), 16), dtype=torch.uint8, device=self.device)
+        self.n_out = int(out_offs[-1])
+
+
+def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan):
+    """scipy.optimize.linear_sum_assignment for every problem of ``plan`` on the GPU.
+    -> (row_ind i64 [n_out], col_ind i64 [n_out], status i32 [n]) device tensors."""
+    dev = cost.device
+    row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
+    col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
+    status = torch.empty(plan.n, dtype=torch.int32, device=dev)
+    torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
+                                     plan.workspace, row_ind, col_ind, status)
+    return row_ind[:plan.n_out], col_ind[:plan.n_out], status

@@ -116,6 +116,27 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                             void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream);
 
 /*
+ * Batched rectangular linear-sum assignment, identical to
+ * scipy.optimize.linear_sum_assignment (the association step of
+ * match_objects, bpc/inference/epipolar_matching.py:100-116, scipy 1.14's
+ * shortest-augmenting-path algorithm, same tie-breaking and output order).
+ * Problem p is the row-major float32 matrix at cost_dev + cost_offs_dev[p]
+ * with dims_dev[2p] rows and dims_dev[2p+1] columns (e.g. the flattened
+ * (N*M, P) cube of mvm_triplet_cost_argmin).  Its min(rows, cols) assigned
+ * (row, col) pairs go to row_ind_dev/col_ind_dev at out_offs_dev[p], sorted
+ * by row; status_dev[p] = 0 ok, 1 NaN/-inf entries, 2 infeasible.
+ * mvm_lsap_plan (HOST arrays, n+1 entries each) fills the per-problem
+ * workspace byte offsets and output offsets and returns the workspace size
+ * (or -1); copy both offset arrays to the device for mvm_lsap_solve.
+ */
+int64_t mvm_lsap_plan(int32_t n_problems, const int64_t *rows, const int64_t *cols,
+                      int64_t *ws_offs, int64_t *out_offs);
+int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const int64_t *dims_dev,
+                   int32_t n_problems, const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
+                   void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
+                   int64_t *col_ind_dev, int32_t *status_dev, mvm_stream_t stream);
+
+/*
  * Diagnostic: fill `bytes` (multiple of 16, 16-byte aligned) of device memory
  * with the same 16-byte nontemporal store stream the residual kernels use.
  * bench.py times it to report the achievable HBM write bandwidth next to the
