@@ -58,6 +58,16 @@ SIGNATURES = {
     "mvm_lsap_solve": (ctypes.c_int, [
         _vp, _vp, _vp, _i32, _vp, _vp,      # cost, cost_offs, dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp, _vp]),     # workspace, bytes, row_ind, col_ind, status, stream
+    "mvm_pack_detections": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
+        ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id
+        _vp, _vp, _vp, _vp, _vp, _vp]),     # counts, cam_offs, pts, boxes_out, status, stream
+    "mvm_triangulate_dlt": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _i32, _vp, _vp]),  # proj, set_of_point, pts2d, n_points, n_views, X, stream
+    "mvm_select_triangulate": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp, _vp,       # cube, cube_offs, cam_offs, lsap_out_offs, row_ind, col_ind
+        _vp, _vp, _i32, ctypes.c_double,    # pts, proj, n_scenes, threshold
+        _vp, _vp, _vp, _vp, _vp]),          # match, cost, X, count, stream
     "mvm_hbm_write_probe": (ctypes.c_int, [_vp, _sz, _vp]),
 }
 

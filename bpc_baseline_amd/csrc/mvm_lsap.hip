@@ -340,8 +340,8 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
     mvm_clear_error();
     if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
     if (n_problems == 0) return MVM_OK;
-    if (!cost_dev || !cost_offs_dev || !dims_dev || !ws_offs_dev || !out_offs_dev ||
-        !row_ind_dev || !col_ind_dev || !status_dev)
+    // cost / row_ind / col_ind may be NULL when every problem is empty
+    if (!cost_offs_dev || !dims_dev || !ws_offs_dev || !out_offs_dev || !status_dev)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     if (!workspace_dev && workspace_bytes)
         return mvm_fail(MVM_ERR_WORKSPACE, "null workspace");

@@ -1,0 +1,121 @@
+"""Batched, device-resident matching of many 3-camera captures.
+
+The reference processes one capture at a time through host Python:
+``PoseEstimator._detect`` packs YOLO boxes into dicts (process_pose.py:116-142),
+``_match`` builds F12/F13/F23, the cost cube, the assignment, the threshold
+filter and the cost sort (:144-183), and ``PosePrediction`` triangulates each
+match (:79-94).  ``match_captures`` runs the same steps for S captures at once
+with every O(n) and larger step on the GPU:
+
+  1. mvm_pack_detections      boxes/conf/cls -> half-integer centroids (CSR)
+  2. host                     F (batched, bit-equal to compute_fundamental_matrix)
+                              and P = K @ RT[:3]; O(1) per capture
+  3. mvm_triplet_cost_argmin  the (N, M, P) cube of every capture
+  4. mvm_lsap_solve           scipy-identical assignment of every flattened cube
+  5. mvm_select_triangulate   cost < threshold, stable sort by cost, DLT
+
+The only device->host transfer before the results is the per-image kept
+count (n_img int32), which sizes the cube and assignment layouts.
+
+Results equal, capture by capture, the reference's ``_match`` outputs fed with
+``_detect``'s detections: match indices and order exactly, ``t`` to rounding
+(tests/test_batch_match_gpu.py).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from .. import ops
+from .utils.camera_utils import camera_pairs, fundamental_matrices_batched
+
+__all__ = ["MatchBatch", "match_captures", "projection_matrices"]
+
+
+def projection_matrices(Ks: np.ndarray, RTs: np.ndarray) -> np.ndarray:
+    """P = K @ RT[:3] per camera (process_pose.py:91: float32 K promoted to
+    float64 by the product with the float64 RT) -> float64 [S, C, 3, 4]."""
+    return np.ascontiguousarray(np.asarray(Ks) @ np.asarray(RTs, dtype=np.float64)[..., :3, :])
+
+
+@dataclass
+class MatchBatch:
+    """Device results of ``match_captures`` (scene s owns rows
+    ``offs[s] : offs[s] + count[s]`` of match / cost / X)."""
+    match: torch.Tensor          # int32 [cap, 3]   (i, j, k) per match
+    cost: torch.Tensor           # float32 [cap]    cube value of the match
+    X: torch.Tensor              # float64 [cap, 3] triangulated centre
+    count: np.ndarray            # int32 [S]
+    offs: np.ndarray             # int64 [S + 1]
+    pts: torch.Tensor            # float64 [n, 2]   packed centroids
+    boxes: torch.Tensor          # int32 [n, 4]     packed int boxes
+    cam_offs: np.ndarray         # int64 [3S + 1]   CSR of pts / boxes
+    cube: Optional[torch.Tensor] = None
+
+    def host(self) -> dict:
+        """One D2H copy of everything ``predictions`` reads."""
+        if not hasattr(self, "_host"):
+            self._host = {k: getattr(self, k).cpu().numpy() for k in ("match", "cost", "X", "pts", "boxes")}
+        return self._host
+
+    def predictions(self, s: int) -> List[tuple]:
+        """Scene s as the reference's PosePrediction fields, in _match's order:
+        list of (boxes int32 [3, 4], centroids f64 [3, 2], t f64 [3])."""
+        o, n = int(self.offs[s]), int(self.count[s])
+        h = self.host()
+        rows = self.cam_offs[3 * s:3 * s + 3][None, :] + h["match"][o:o + n].astype(np.int64)
+        return [(h["boxes"][rows[q]], h["pts"][rows[q]], h["X"][o + q]) for q in range(n)]
+
+
+def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
+                   img_offs: torch.Tensor, Ks: np.ndarray, RTs: np.ndarray, *,
+                   conf_thresh: float = 0.1, matching_threshold: float = 30,
+                   keep_cube: bool = False) -> MatchBatch:
+    """Detect-packing + matching + triangulation of S 3-camera captures.
+
+    ``boxes`` f32 [n, 4] xyxy, ``conf``/``cls`` f32 [n]: the detector outputs
+    of the 3S images (capture s, camera c = image 3s + c) concatenated on the
+    device; ``img_offs`` int64 [3S + 1] device.  ``Ks`` float32 [S, 3, 3, 3],
+    ``RTs`` float64 [S, 3, 4, 4] (host).  Defaults are PoseEstimatorParams'
+    (process_pose.py:36-37).
+    """
+    dev = boxes.device
+    n_img = int(img_offs.numel()) - 1
+    if n_img % 3:
+        raise ValueError("img_offs must describe 3 images per capture")
+    S = n_img // 3
+    Ks = np.asarray(Ks, dtype=np.float32).reshape(S, 3, 3, 3)
+    RTs = np.asarray(RTs, dtype=np.float64).reshape(S, 3, 4, 4)
+
+    pts, cam_offs, boxes_int, counts, status = ops.pack_detections(boxes, conf, cls, img_offs,
+                                                                   conf_thresh)
+    # host work while the packing runs: F and P for every capture
+    F = fundamental_matrices_batched(Ks, RTs, camera_pairs(3))
+    F_dev = torch.from_numpy(F.reshape(-1)).to(dev, non_blocking=False)
+    proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev)
+
+    counts_host = counts.cpu().numpy().astype(np.int64)
+    if int(status.item()) != 0:
+        raise ValueError("detector box with a non-finite or out-of-range coordinate")
+    cam_offs_host = np.zeros(n_img + 1, np.int64)
+    np.cumsum(counts_host, out=cam_offs_host[1:])
+
+    plan = ops.TripletPlan(cam_offs_host, S, device=dev)
+    cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan)
+    c3 = counts_host.reshape(S, 3)
+    lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+    row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(cube, plan.cube_offs[:-1].contiguous(),
+                                                                lplan)
+    match, cost, X, count = ops.select_triangulate(cube, plan.cube_offs, cam_offs, lplan.out_offs,
+                                                   row_ind, col_ind, pts, proj_dev,
+                                                   float(matching_threshold))
+    bad = lstat.cpu().numpy()
+    if np.any(bad):
+        raise ValueError(f"assignment failed for captures {np.nonzero(bad)[0][:8].tolist()} "
+                         "(cost matrix contains invalid numeric entries or is infeasible)")
+    return MatchBatch(match=match, cost=cost, X=X, count=count.cpu().numpy(),
+                      offs=lplan.out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
+                      cube=cube if keep_cube else None)

@@ -28,6 +28,7 @@ __all__ = [
     "PairwisePlan", "TripletPlan",
     "pairwise_residual_argmin", "pairwise_residual_f64", "triplet_cost_argmin",
     "hbm_write_probe", "LsapPlan", "linear_sum_assignment_batched",
+    "pack_detections", "triangulate_dlt", "select_triangulate",
 ]
 
 
@@ -159,6 +160,111 @@ def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tenso
 
 @lsap_solve_out.register_fake
 def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status):
+    return None
+
+
+@torch.library.custom_op("mvmatch::pack_detections_out",
+                         mutates_args=("counts", "cam_offs", "pts", "boxes_out", "status"))
+def pack_detections_out(boxes: Tensor, conf: Tensor, cls: Tensor, img_offs: Tensor,
+                        conf_thresh: float, class_id: float, counts: Tensor, cam_offs: Tensor,
+                        pts: Tensor, boxes_out: Tensor, status: Tensor) -> None:
+    dev = boxes.device
+    if dev.type != "cuda":
+        raise ValueError("boxes must be a GPU tensor (the packer has no CPU path)")
+    n_img = counts.numel()
+    n = boxes.shape[0] if boxes.dim() == 2 else -1
+    if boxes.dim() != 2 or boxes.shape[1] != 4:
+        raise ValueError("boxes must be [n, 4] (xyxy)")
+    for t, name, dt, numel in ((boxes, "boxes", torch.float32, 4 * n), (conf, "conf", torch.float32, n),
+                               (cls, "cls", torch.float32, n), (img_offs, "img_offs", torch.int64, n_img + 1),
+                               (counts, "counts", torch.int32, n_img),
+                               (cam_offs, "cam_offs", torch.int64, n_img + 1),
+                               (pts, "pts", torch.float64, 2 * n),
+                               (boxes_out, "boxes_out", torch.int32, 4 * n), (status, "status", torch.int32, 1)):
+        _require(t, name, dt, dev)
+        if t.numel() < numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, needs {numel}")
+    st = _native.load().mvm_pack_detections(_p(boxes), _p(conf), _p(cls), _p(img_offs), n_img,
+                                            float(conf_thresh), float(class_id), _p(counts),
+                                            _p(cam_offs), _p(pts), _p(boxes_out), _p(status),
+                                            _stream(boxes))
+    _native.check("mvm_pack_detections", st)
+
+
+@pack_detections_out.register_fake
+def _(boxes, conf, cls, img_offs, conf_thresh, class_id, counts, cam_offs, pts, boxes_out, status):
+    return None
+
+
+@torch.library.custom_op("mvmatch::triangulate_dlt_out", mutates_args=("X",))
+def triangulate_dlt_out(proj: Tensor, set_of_point: Optional[Tensor], pts2d: Tensor,
+                        X: Tensor) -> None:
+    dev = pts2d.device
+    if dev.type != "cuda":
+        raise ValueError("pts2d must be a GPU tensor (the triangulator has no CPU path)")
+    if pts2d.dim() != 3 or pts2d.shape[2] != 2:
+        raise ValueError("pts2d must be [n_points, n_views, 2]")
+    n_points, n_views = int(pts2d.shape[0]), int(pts2d.shape[1])
+    _require(pts2d, "pts2d", torch.float64, dev)
+    _require(proj, "proj", torch.float64, dev)
+    _require(X, "X", torch.float64, dev)
+    if proj.dim() != 4 or tuple(proj.shape[1:]) != (n_views, 3, 4):
+        raise ValueError("proj must be [n_sets, n_views, 3, 4]")
+    if X.numel() < 3 * n_points:
+        raise ValueError("X must hold [n_points, 3]")
+    if set_of_point is None:
+        if proj.shape[0] < n_points:
+            raise ValueError("without set_of_point, proj needs one set per point")
+    else:
+        _require(set_of_point, "set_of_point", torch.int32, dev)
+        if set_of_point.numel() != n_points:
+            raise ValueError("set_of_point must have n_points entries")
+    st = _native.load().mvm_triangulate_dlt(_p(proj), _p(set_of_point), _p(pts2d), n_points,
+                                            n_views, _p(X), _stream(pts2d))
+    _native.check("mvm_triangulate_dlt", st)
+
+
+@triangulate_dlt_out.register_fake
+def _(proj, set_of_point, pts2d, X):
+    return None
+
+
+@torch.library.custom_op("mvmatch::select_triangulate_out",
+                         mutates_args=("match", "cost", "X", "count"))
+def select_triangulate_out(cube: Tensor, cube_offs: Tensor, cam_offs: Tensor, lsap_offs: Tensor,
+                           row_ind: Tensor, col_ind: Tensor, pts: Tensor, proj: Tensor,
+                           threshold: float, match: Tensor, cost: Tensor, X: Tensor,
+                           count: Tensor) -> None:
+    dev = cube.device
+    if dev.type != "cuda":
+        raise ValueError("cube must be a GPU tensor (the matcher has no CPU path)")
+    n_scenes = count.numel()
+    for t, name, dt, numel in ((cube, "cube", torch.float32, 0),
+                               (cube_offs, "cube_offs", torch.int64, n_scenes + 1),
+                               (cam_offs, "cam_offs", torch.int64, 3 * n_scenes + 1),
+                               (lsap_offs, "lsap_offs", torch.int64, n_scenes + 1),
+                               (row_ind, "row_ind", torch.int64, 0), (col_ind, "col_ind", torch.int64, 0),
+                               (pts, "pts", torch.float64, 0), (proj, "proj", torch.float64, 36 * n_scenes),
+                               (match, "match", torch.int32, 3 * row_ind.numel()),
+                               (cost, "cost", torch.float32, row_ind.numel()),
+                               (X, "X", torch.float64, 3 * row_ind.numel()),
+                               (count, "count", torch.int32, 0)):
+        _require(t, name, dt, dev)
+        if numel and t.numel() != numel and name in ("cube_offs", "cam_offs", "lsap_offs", "proj"):
+            raise ValueError(f"{name} holds {t.numel()} elements, expected {numel}")
+        if numel and t.numel() < numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, needs {numel}")
+    if col_ind.numel() != row_ind.numel():
+        raise ValueError("row_ind / col_ind differ in length")
+    st = _native.load().mvm_select_triangulate(
+        _p(cube), _p(cube_offs), _p(cam_offs), _p(lsap_offs), _p(row_ind), _p(col_ind), _p(pts),
+        _p(proj), n_scenes, float(threshold), _p(match), _p(cost), _p(X), _p(count), _stream(cube))
+    _native.check("mvm_select_triangulate", st)
+
+
+@select_triangulate_out.register_fake
+def _(cube, cube_offs, cam_offs, lsap_offs, row_ind, col_ind, pts, proj, threshold, match, cost,
+      X, count):
     return None
 
 
@@ -319,3 +425,56 @@ def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPla
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
                                      plan.workspace, row_ind, col_ind, status)
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
+
+
+def pack_detections(boxes: Tensor, conf: Tensor, cls: Tensor, img_offs: Tensor,
+                    conf_thresh: float, class_id: float = 0.0):
+    """PoseEstimator._detect's box filtering + centres for a batch of images, on device.
+
+    ``boxes`` f32 [n, 4] xyxy, ``conf``/``cls`` f32 [n] of all images
+    concatenated, image k owning rows ``img_offs[k]:img_offs[k+1]`` (int64
+    device tensor).  The threshold is rounded to float32 first, as numpy does
+    when comparing a float32 array with a Python float (process_pose.py:130).
+    -> (pts f64 [n, 2], cam_offs i64 [n_img+1], boxes_int i32 [n, 4],
+    counts i32 [n_img], status i32 [1]) — rows past ``cam_offs[-1]`` are
+    unused capacity; the matcher reads only the rows the offsets name.
+    """
+    dev = boxes.device
+    n = int(boxes.shape[0])
+    n_img = int(img_offs.numel()) - 1
+    counts = torch.empty(max(n_img, 0), dtype=torch.int32, device=dev)
+    cam_offs = torch.zeros(max(n_img, 0) + 1, dtype=torch.int64, device=dev)
+    pts = torch.empty((n, 2), dtype=torch.float64, device=dev)
+    boxes_out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    thresh = float(np.float32(conf_thresh))
+    torch.ops.mvmatch.pack_detections_out(boxes.contiguous(), conf.contiguous(), cls.contiguous(),
+                                          img_offs, thresh, float(np.float32(class_id)), counts,
+                                          cam_offs, pts, boxes_out, status)
+    return pts, cam_offs, boxes_out, counts, status
+
+
+def triangulate_dlt(proj: Tensor, pts2d: Tensor, set_of_point: Optional[Tensor] = None) -> Tensor:
+    """triangulate_multi_view for every point at once -> X f64 [n_points, 3] (device)."""
+    X = torch.empty((int(pts2d.shape[0]), 3), dtype=torch.float64, device=pts2d.device)
+    torch.ops.mvmatch.triangulate_dlt_out(proj.contiguous(), set_of_point, pts2d.contiguous(), X)
+    return X
+
+
+def select_triangulate(cube: Tensor, cube_offs: Tensor, cam_offs: Tensor, lsap_offs: Tensor,
+                       row_ind: Tensor, col_ind: Tensor, pts: Tensor, proj: Tensor,
+                       threshold: float):
+    """Filter + stable cost sort + DLT of every scene's assignment (device).
+    -> (match i32 [cap, 3], cost f32 [cap], X f64 [cap, 3], count i32 [S]); scene
+    s's matches are rows ``lsap_offs[s] : lsap_offs[s] + count[s]``."""
+    dev = cube.device
+    cap = int(row_ind.numel())
+    n_scenes = int(lsap_offs.numel()) - 1
+    match = torch.empty((cap, 3), dtype=torch.int32, device=dev)
+    cost = torch.empty(cap, dtype=torch.float32, device=dev)
+    X = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    count = torch.empty(n_scenes, dtype=torch.int32, device=dev)
+    torch.ops.mvmatch.select_triangulate_out(cube, cube_offs, cam_offs, lsap_offs, row_ind,
+                                             col_ind, pts, proj.contiguous(), float(threshold),
+                                             match, cost, X, count)
+    return match, cost, X, count

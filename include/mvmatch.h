@@ -137,6 +137,61 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
                    int64_t *col_ind_dev, int32_t *status_dev, mvm_stream_t stream);
 
 /*
+ * On-device detection packing, replacing the per-box loop of
+ * PoseEstimator._detect (bpc/inference/process_pose.py:122-140).  Input:
+ * the detector's boxes of n_img images in CSR form: boxes_dev f32 [n, 4]
+ * (xyxy), conf_dev f32 [n], cls_dev f32 [n], image k owning rows
+ * [img_offs_dev[k], img_offs_dev[k+1]).  A box is kept when cls == class_id
+ * and conf >= conf_thresh (both float32 compares, :130), in input order.
+ * Output, the matcher's CSR input: counts_dev int32 [n_img],
+ * cam_offs_dev int64 [n_img+1] (exclusive prefix of counts), boxes_out_dev
+ * int32 [kept, 4] = int(box) (truncation toward zero, :134) and pts_dev f64
+ * [kept, 2] = 0.5 * (x1 + x2), 0.5 * (y1 + y2) (:135-136).  Capacity of the
+ * two row outputs must be img_offs[n_img] rows.  status_dev[0] = 1 if a kept
+ * box had a non-finite coordinate or one with |x| >= 2^30 (stored as 0).
+ */
+int mvm_pack_detections(const float *boxes_dev, const float *conf_dev, const float *cls_dev,
+                        const int64_t *img_offs_dev, int32_t n_img, float conf_thresh,
+                        float class_id, int32_t *counts_dev, int64_t *cam_offs_dev,
+                        double *pts_dev, int32_t *boxes_out_dev, int32_t *status_dev,
+                        mvm_stream_t stream);
+
+/*
+ * Batched DLT triangulation, replacing triangulate_multi_view
+ * (bpc/inference/epipolar_matching.py:118-127) as called per match by
+ * PosePrediction.triangulate (process_pose.py:86-94).  Point p uses the
+ * n_views projection matrices (f64, row-major 3x4) of set
+ * set_of_point_dev[p] (or set p when NULL) at proj_dev + set*n_views*12 and
+ * its 2-D points pts2d_dev [n_points, n_views, 2]; X_dev [n_points, 3] =
+ * X[:3] / X[3] of the right singular vector of the smallest singular value
+ * of the 2V x 4 system.  fp64; agrees with LAPACK to rounding (the vector is
+ * unique up to sign, which the division cancels).  2 <= n_views <= 8.
+ */
+int mvm_triangulate_dlt(const double *proj_dev, const int32_t *set_of_point_dev,
+                        const double *pts2d_dev, int32_t n_points, int32_t n_views, double *X_dev,
+                        mvm_stream_t stream);
+
+/*
+ * The tail of PoseEstimator._match (process_pose.py:182-187) for a batch of
+ * 3-camera scenes, after mvm_triplet_cost_argmin and mvm_lsap_solve: scene
+ * s's assignment (row_ind/col_ind at lsap_out_offs_dev[s], the flattened
+ * (N*M, P) cube at cube_offs_dev[s]) is filtered by cube value < threshold
+ * (match_objects :111; compared in float64, as numpy 1.26 compares a float32
+ * scalar with a Python number), decoded i = r / M, j = r % M, k = c
+ * (:112-114), stably sorted by cost (:183) and triangulated from the
+ * centroids pts_dev (CSR cam_offs_dev, 3 views per scene) with the scene's
+ * projection matrices proj_dev [S, 3, 3, 4] (K @ RT[:3], :86-94).  Match w
+ * of scene s (w < count_dev[s]) is written at lsap_out_offs_dev[s] + w:
+ * match_dev int32 [.., 3] = (i, j, k), cost_dev f32, X_dev f64 [.., 3].
+ */
+int mvm_select_triangulate(const float *cube_dev, const int64_t *cube_offs_dev,
+                           const int64_t *cam_offs_dev, const int64_t *lsap_out_offs_dev,
+                           const int64_t *row_ind_dev, const int64_t *col_ind_dev,
+                           const double *pts_dev, const double *proj_dev, int32_t n_scenes,
+                           double threshold, int32_t *match_dev, float *cost_dev, double *X_dev,
+                           int32_t *count_dev, mvm_stream_t stream);
+
+/*
  * Diagnostic: fill `bytes` (multiple of 16, 16-byte aligned) of device memory
  * with the same 16-byte nontemporal store stream the residual kernels use.
  * bench.py times it to report the achievable HBM write bandwidth next to the

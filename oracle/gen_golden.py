@@ -17,6 +17,9 @@ Fixtures (all .npz, loaded with allow_pickle=False):
   a5_pairwise.npz        4-camera pairwise residual matrices (f32 of epipolar_error)
   a6_fundamental.npz     compute_fundamental_matrix on IPD-like rigs
   a7_match.npz           PoseEstimator._match on synthetic captures (matches, t)
+  a8_detect.npz          PoseEstimator._detect box packing, detector replaced by a stub
+                         returning synthetic boxes/confidences/classes
+  a9_triangulate.npz     triangulate_multi_view on 2/3/4/8-view systems
 
 Run: python oracle/gen_golden.py [--reference /root/reference]
 """
@@ -237,18 +240,135 @@ def gen_a7(pp, rng):
     np.savez_compressed(os.path.join(OUT, "a7_match.npz"), **arrays)
 
 
+class _StubBoxes:
+    """What _detect reads from a YOLO result (process_pose.py:126-129)."""
+
+    def __init__(self, xyxy, conf, cls):
+        import torch
+        self.xyxy = torch.from_numpy(xyxy)
+        self.conf = torch.from_numpy(conf)
+        self.cls = torch.from_numpy(cls)
+
+    def __len__(self):
+        return int(self.xyxy.shape[0])
+
+
+class _StubYolo:
+    def __init__(self, per_image):
+        self.per_image = list(per_image)
+
+    def __call__(self, image, imgsz=None):
+        return [types.SimpleNamespace(boxes=_StubBoxes(*self.per_image.pop(0)))]
+
+
+def _synthetic_yolo_outputs(rng, n_img, thresh):
+    """Boxes with fractional, integral, negative and near-integer coordinates;
+    confidences straddling the float32 threshold; classes 0/1/2."""
+    out = []
+    t32 = np.float32(thresh)
+    for _ in range(n_img):
+        n = int(rng.choice([0, 1, 3, 17, 40, 300]))
+        x1 = rng.uniform(-4.0, 1900.0, n)
+        y1 = rng.uniform(-4.0, 1100.0, n)
+        w = rng.uniform(0.0, 300.0, n)
+        h = rng.uniform(0.0, 300.0, n)
+        xyxy = np.stack([x1, y1, x1 + w, y1 + h], axis=1).astype(np.float32)
+        sel = rng.random(xyxy.shape) < 0.15
+        xyxy[sel] = np.round(xyxy[sel])                               # exact integers
+        sel = rng.random(xyxy.shape) < 0.1
+        xyxy[sel] = np.nextafter(np.round(xyxy[sel]), np.float32(-np.inf))  # 5.9999995 etc.
+        sel = rng.random(xyxy.shape) < 0.05
+        xyxy[sel] = -rng.uniform(0.0, 0.999, int(sel.sum())).astype(np.float32)  # int() -> 0
+        conf = rng.uniform(0.0, 1.0, n).astype(np.float32)
+        pick = rng.random(n)
+        conf[pick < 0.1] = t32
+        conf[(pick >= 0.1) & (pick < 0.2)] = np.nextafter(t32, np.float32(-np.inf))
+        cls = rng.choice(np.asarray([0.0, 0.0, 0.0, 1.0, 2.0], np.float32), n)
+        out.append((xyxy, conf, cls))
+    return out
+
+
+def gen_a8(pp, rng):
+    """PoseEstimator._detect (process_pose.py:116-142) with the detector stubbed."""
+    est = pp.PoseEstimator.__new__(pp.PoseEstimator)
+    arrays = {}
+    sets = [(0.1, 12), (0.25, 9), (0.5, 6)]
+    for c, (thresh, n_img) in enumerate(sets):
+        est.params = pp.PoseEstimatorParams(yolo_conf_thresh=thresh)
+        raw = _synthetic_yolo_outputs(rng, n_img, thresh)
+        est.yolo = _StubYolo(raw)
+        capture = types.SimpleNamespace(images=[np.zeros((4, 4, 3), np.uint8)] * n_img)
+        preds = est._detect(capture)
+        in_offs = np.zeros(n_img + 1, np.int64)
+        out_offs = np.zeros(n_img + 1, np.int64)
+        in_offs[1:] = np.cumsum([r[0].shape[0] for r in raw])
+        out_offs[1:] = np.cumsum([len(preds[k]) for k in range(n_img)])
+        arrays[f"d{c}_thresh"] = np.asarray(thresh)
+        arrays[f"d{c}_in_offs"] = in_offs
+        arrays[f"d{c}_boxes"] = np.concatenate([r[0] for r in raw]).reshape(-1, 4)
+        arrays[f"d{c}_conf"] = np.concatenate([r[1] for r in raw])
+        arrays[f"d{c}_cls"] = np.concatenate([r[2] for r in raw])
+        arrays[f"d{c}_out_offs"] = out_offs
+        arrays[f"d{c}_bbox"] = np.concatenate(
+            [_boxes_array(preds[k]) for k in range(n_img)]).reshape(-1, 4)
+        arrays[f"d{c}_center"] = np.concatenate(
+            [_dets_array(preds[k]) for k in range(n_img)]).reshape(-1, 2)
+        print(f"a8: thresh {thresh}: {n_img} images, {in_offs[-1]} boxes, {out_offs[-1]} kept")
+    arrays["n"] = np.asarray(len(sets))
+    np.savez_compressed(os.path.join(OUT, "a8_detect.npz"), **arrays)
+
+
+def gen_a9(em, rng):
+    """triangulate_multi_view (epipolar_matching.py:118-127): projections of
+    random points through IPD-like rigs, with pixel noise, 2-8 views."""
+    from bpc_baseline_amd.synth import make_rig
+    arrays = {}
+    for V in (2, 3, 4, 8):
+        n = 64
+        proj = np.empty((n, V, 3, 4))
+        pts = np.empty((n, V, 2))
+        X = np.empty((n, 3))
+        for q in range(n):
+            Ks, RTs = make_rig(rng, V)
+            P = np.stack([Ks[v] @ RTs[v][:3] for v in range(V)])
+            Xw = np.array([*rng.uniform(-250.0, 250.0, 2), rng.uniform(-80.0, 80.0), 1.0])
+            uvw = P @ Xw
+            uv = uvw[:, :2] / uvw[:, 2:3]
+            # centroids are half-integers in the pipeline (0.5 * (x1 + x2))
+            uv = np.round(2.0 * (uv + rng.normal(0.0, 2.0, uv.shape))) / 2.0
+            proj[q], pts[q] = P, uv
+            X[q] = em.triangulate_multi_view(list(P), uv)
+        arrays[f"v{V}_proj"], arrays[f"v{V}_pts"], arrays[f"v{V}_X"] = proj, pts, X
+        print(f"a9: {n} {V}-view systems")
+    np.savez_compressed(os.path.join(OUT, "a9_triangulate.npz"), **arrays)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default="", help="comma list, e.g. a8,a9 (default: all)")
     args = ap.parse_args()
     os.makedirs(OUT, exist_ok=True)
     em, cu, pp = _import_reference(args.reference)
+    only = set(filter(None, args.only.split(",")))
+    want = (lambda k: not only or k in only)
     rng = np.random.default_rng(20250509)
-    gen_a1(em, rng)
-    gen_a3(em, rng)
-    gen_a5(em, rng)
-    gen_a6(cu, rng)
-    gen_a7(pp, rng)
+    if want("a1"):
+        gen_a1(em, rng)
+    if want("a3"):
+        gen_a3(em, rng)
+    if want("a5"):
+        gen_a5(em, rng)
+    if want("a6"):
+        gen_a6(cu, rng)
+    if want("a7"):
+        gen_a7(pp, rng)
+    # a8/a9 draw from their own stream so a1-a7 stay reproducible on their own
+    rng2 = np.random.default_rng(20250510)
+    if want("a8"):
+        gen_a8(pp, rng2)
+    if want("a9"):
+        gen_a9(em, rng2)
 
 
 if __name__ == "__main__":

@@ -96,3 +96,22 @@ def test_check_raises(lib):
         st = lib.mvm_pairwise_residual_argmin(FAKE, FAKE, FAKE, pa, pb, 1, 99, 1, 4,
                                               FAKE, FAKE, FAKE, FAKE, FAKE, None)
         _native.check("mvm_pairwise_residual_argmin", st)
+
+
+def test_pack_detections_validation(lib):
+    f = ctypes.c_float
+    # no images: nothing launched; negative count and missing offsets refused
+    assert lib.mvm_pack_detections(None, None, None, None, 0, f(0.1), f(0.0), None, None, None,
+                                   None, None, None) == 0
+    assert lib.mvm_pack_detections(None, None, None, FAKE, -1, f(0.1), f(0.0), FAKE, FAKE, None,
+                                   None, FAKE, None) == 1
+    assert lib.mvm_pack_detections(FAKE, FAKE, FAKE, None, 3, f(0.1), f(0.0), FAKE, FAKE, FAKE,
+                                   FAKE, FAKE, None) == 1
+
+
+def test_triangulate_dlt_validation(lib):
+    assert lib.mvm_triangulate_dlt(None, None, None, 0, 3, None, None) == 0
+    assert lib.mvm_triangulate_dlt(FAKE, None, FAKE, 5, 1, FAKE, None) == 1      # one view
+    assert lib.mvm_triangulate_dlt(FAKE, None, FAKE, 5, 9, FAKE, None) == 1      # > MVM_MAX_CAMS
+    assert b"n_views" in lib.mvm_last_error_string()
+    assert lib.mvm_triangulate_dlt(None, None, FAKE, 5, 3, FAKE, None) == 1

@@ -82,6 +82,16 @@ def test_ops_reject_cpu_tensors():
                                      plan)
 
 
+def test_pipeline_ops_reject_cpu_tensors():
+    from bpc_baseline_amd import ops
+    with pytest.raises(ValueError, match="GPU"):
+        ops.pack_detections(torch.zeros(2, 4), torch.ones(2), torch.zeros(2),
+                            torch.tensor([0, 2]), 0.1)
+    with pytest.raises(ValueError, match="GPU"):
+        ops.triangulate_dlt(torch.zeros(1, 3, 3, 4, dtype=torch.float64),
+                            torch.zeros(1, 3, 2, dtype=torch.float64))
+
+
 @pytest.mark.skipif(torch.cuda.is_available(), reason="checks the no-GPU failure mode")
 def test_dropin_fails_loudly_without_gpu():
     from bpc_baseline_amd.inference import epipolar_matching as em
