@@ -167,3 +167,73 @@ def test_full_c2_cube_slice_bit_exact(cuda):
     rc, ra, rm, _, _ = O.cube(b.pts, b.cam_offs, b.F, b.n_scenes)
     assert np.array_equal(c.cpu().numpy().view(np.int32), rc.view(np.int32))
     assert np.array_equal(a.cpu().numpy(), ra)
+
+
+class _StubBoxes:
+    def __init__(self, xyxy, conf, cls, dev):
+        self.xyxy = torch.from_numpy(np.ascontiguousarray(xyxy, np.float32)).to(dev)
+        self.conf = torch.from_numpy(np.ascontiguousarray(conf, np.float32)).to(dev)
+        self.cls = torch.from_numpy(np.ascontiguousarray(cls, np.float32)).to(dev)
+
+    def __len__(self):
+        return int(self.xyxy.shape[0])
+
+
+class _StubYolo:
+    """Stands in for ultralytics.YOLO: returns canned boxes on the GPU, as the
+    real detector's results.boxes hold them."""
+
+    def __init__(self, per_image, dev):
+        self.per_image, self.dev = list(per_image), dev
+
+    def __call__(self, image, imgsz=None):
+        return [types.SimpleNamespace(boxes=_StubBoxes(*self.per_image.pop(0), self.dev))]
+
+
+def test_detect_dropin_equals_reference(cuda, golden):
+    """MatcherMixin._detect == the reference _detect (a8, detector stubbed the same way)."""
+    from bpc_baseline_amd.inference import process_pose as pp
+    z = golden("a8_detect.npz")
+    for c in range(int(z["n"])):
+        o = z[f"d{c}_in_offs"]
+        raw = [(z[f"d{c}_boxes"][o[k]:o[k + 1]], z[f"d{c}_conf"][o[k]:o[k + 1]],
+                z[f"d{c}_cls"][o[k]:o[k + 1]]) for k in range(len(o) - 1)]
+        est = pp.MatcherMixin()
+        est.yolo = _StubYolo(raw, cuda)
+        est.params = pp.PoseEstimatorParams(yolo_conf_thresh=float(z[f"d{c}_thresh"]))
+        cap = types.SimpleNamespace(images=[np.zeros((4, 4, 3), np.uint8)] * (len(o) - 1))
+        dets = est._detect(cap)
+        oo = z[f"d{c}_out_offs"]
+        for k in range(len(o) - 1):
+            want = [{"bbox": tuple(int(v) for v in b), "bb_center": tuple(float(v) for v in q)}
+                    for b, q in zip(z[f"d{c}_bbox"][oo[k]:oo[k + 1]], z[f"d{c}_center"][oo[k]:oo[k + 1]])]
+            assert dets[k] == want
+            for d in dets[k]:
+                assert all(type(v) is int for v in d["bbox"])
+                assert all(type(v) is float for v in d["bb_center"])
+
+
+def test_detect_then_match_dropin(cuda, golden):
+    """_detect -> _match through the packed device centroids == the reference (a7)."""
+    from bpc_baseline_amd.inference import process_pose as pp
+    z = golden("a7_match.npz")
+    for c in range(int(z["n"])):
+        raw = []
+        for cam in range(3):
+            b = z[f"m{c}_boxes{cam}"].astype(np.float32)
+            b = np.where(b >= 0, b + np.float32(0.25), b - np.float32(0.25))  # int() truncates
+            raw.append((b, np.ones(len(b)), np.zeros(len(b))))
+        est = pp.MatcherMixin()
+        est.yolo = _StubYolo(raw, cuda)
+        est.params = pp.PoseEstimatorParams()
+        cap = types.SimpleNamespace(images=[np.zeros((4, 4, 3), np.uint8)] * 3,
+                                    Ks=list(z[f"m{c}_K"]), RTs=list(z[f"m{c}_RT"]))
+        dets = est._detect(cap)
+        assert isinstance(dets, pp.PackedDetections)
+        np.random.seed(1234 + c)
+        preds = est._match(cap, dets)
+        assert len(preds) == z[f"m{c}_t"].shape[0]
+        for q, p in enumerate(preds):
+            np.testing.assert_array_equal(p.boxes, z[f"m{c}_boxes"][q])
+            np.testing.assert_array_equal(p.centroids, z[f"m{c}_centroids"][q])
+            np.testing.assert_allclose(p.t, z[f"m{c}_t"][q], rtol=1e-12, atol=1e-9)
