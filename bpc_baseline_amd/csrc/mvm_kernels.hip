@@ -169,10 +169,14 @@ typedef f32x4 __attribute__((address_space(1))) g_f32x4;   // global (AS 1) poin
 // Row store from a scalar (SGPR) row address + a 32-bit per-lane byte offset:
 // lowers to `global_store_dwordx4 v_off, v_data, s_base nt` (saddr form, no
 // per-row 64-bit VALU address arithmetic).
+template <bool NT = true>
 __device__ __forceinline__ void store4_nt_row(uint64_t row_base, uint32_t byte_off,
                                               const float v4[4]) {
     const f32x4 v = {v4[0], v4[1], v4[2], v4[3]};
-    __builtin_nontemporal_store(v, reinterpret_cast<g_f32x4 *>(row_base + byte_off));
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<g_f32x4 *>(row_base + byte_off));
+    else
+        *reinterpret_cast<g_f32x4 *>(row_base + byte_off) = v;
 }
 __device__ __forceinline__ void store4_nt(double *dst, const double e[4]) {
     const f64x2 lo = {e[0], e[1]}, hi = {e[2], e[3]};
@@ -266,7 +270,7 @@ __device__ __forceinline__ uint32_t best_key(const Best &b) {
 
 // One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
 // per pair, one 16-byte store, 3 int ops of argmin per pair.
-template <bool ARGMIN, bool STORE, typename OutT>
+template <bool ARGMIN, bool STORE, typename OutT, bool NT = true>
 __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, OutT *drow, int jbase, Best &best) {
     double e[kColsPerLane];
@@ -283,7 +287,7 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
         }
     }
     if constexpr (sizeof(OutT) == 4) {
-        if (STORE) store4_nt_row(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+        if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
         if (ARGMIN) {
 #pragma unroll
             for (int q = 0; q < kColsPerLane; ++q) best_update_fast(best, v[q], jbase + q);
@@ -316,7 +320,7 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
-template <int RPW, bool ARGMIN, typename OutT>
+template <int RPW, bool ARGMIN, typename OutT, bool NT = true>
 __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
@@ -442,7 +446,7 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        row_fast<ARGMIN, true>(c, s_row[wave][r][0], s_row[wave][r][1],
+                        row_fast<ARGMIN, true, OutT, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
                                                s_row[wave][r][2], s_row[wave][r][3],
                                                s_row[wave][r][4], reinterpret_cast<OutT *>(rp),
                                                jbase, best[r]);
@@ -927,13 +931,35 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
 // Speed-of-light reference for the roofline: every workgroup writes one
 // contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
 // wave instruction 1 KiB contiguous) -- the store form of the residual kernels.
+template <int PER_LANE, bool NT>
 __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_t n16, float val) {
     const f32x4 v = {val, val, val, val};
-    const size_t base = (size_t)blockIdx.x * (4 * kThreads) + threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * (PER_LANE * kThreads) + threadIdx.x;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < PER_LANE; ++k) {
         const size_t i = base + (size_t)k * kThreads;
-        if (i < n16) __builtin_nontemporal_store(v, dst + i);
+        if (i < n16) {
+            if (NT) __builtin_nontemporal_store(v, dst + i);
+            else dst[i] = v;
+        }
+    }
+}
+
+// grid-stride variant: a fixed grid of `waves per CU` x 256 CUs workgroups
+template <bool NT>
+__global__ __launch_bounds__(kThreads) void write_probe_stride_kernel(f32x4 *dst, size_t n16,
+                                                                      float val) {
+    const f32x4 v = {val, val, val, val};
+    const size_t step = (size_t)gridDim.x * kThreads * 4;
+    for (size_t b = (size_t)blockIdx.x * kThreads * 4 + threadIdx.x; b < n16; b += step) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const size_t i = b + (size_t)k * kThreads;
+            if (i < n16) {
+                if (NT) __builtin_nontemporal_store(v, dst + i);
+                else dst[i] = v;
+            }
+        }
     }
 }
 
@@ -996,10 +1022,12 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg);
     if (f64) {
         pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
-    } else if (argmin) {
-        pairwise_kernel<RPW, true, float><<<grid, block, lds, stream>>>(a);
+    } else if (env_int("MVM_PAIRWISE_NT", 1)) {
+        if (argmin) pairwise_kernel<RPW, true, float, true><<<grid, block, lds, stream>>>(a);
+        else pairwise_kernel<RPW, false, float, true><<<grid, block, lds, stream>>>(a);
     } else {
-        pairwise_kernel<RPW, false, float><<<grid, block, lds, stream>>>(a);
+        if (argmin) pairwise_kernel<RPW, true, float, false><<<grid, block, lds, stream>>>(a);
+        else pairwise_kernel<RPW, false, float, false><<<grid, block, lds, stream>>>(a);
     }
 }
 
@@ -1145,11 +1173,24 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
     if (!dst_dev || (((uintptr_t)dst_dev) & 15) || (bytes & 15))
         return fail(MVM_ERR_INVALID_ARGUMENT, "write probe needs a 16-byte aligned buffer/size");
     const size_t n16 = bytes / 16;
-    const size_t blocks = (n16 + 4 * kThreads - 1) / (4 * kThreads);
+    // MVM_PROBE_MODE (experiments): 0 nt 16 KiB/WG (the residual kernels' form),
+    // 1 plain 16 KiB/WG, 2 nt 64 KiB/WG, 3 plain 64 KiB/WG, 4 nt grid-stride, 5 plain grid-stride
+    const int mode = env_int("MVM_PROBE_MODE", 0);
+    const int per = (mode == 2 || mode == 3) ? 16 : 4;
+    const size_t blocks = (n16 + per * kThreads - 1) / (per * kThreads);
     if (blocks == 0) return MVM_OK;
     if (blocks > 0x7FFFFFFFull) return fail(MVM_ERR_UNSUPPORTED, "write probe buffer too large");
-    write_probe_kernel<<<(unsigned)blocks, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        reinterpret_cast<f32x4 *>(dst_dev), n16, 1.0f);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    f32x4 *d = reinterpret_cast<f32x4 *>(dst_dev);
+    const unsigned stride_grid = (unsigned)env_int("MVM_PROBE_GRID", 256 * 8);
+    switch (mode) {
+        case 1: write_probe_kernel<4, false><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 2: write_probe_kernel<16, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 3: write_probe_kernel<16, false><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 4: write_probe_stride_kernel<true><<<stride_grid, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 5: write_probe_stride_kernel<false><<<stride_grid, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        default: write_probe_kernel<4, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+    }
     return check_launch("write_probe_kernel");
 }
 

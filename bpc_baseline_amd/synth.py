@@ -172,3 +172,60 @@ def make_scenes(n_scenes: int, n_cams: int, n_dets, *, seed: int = 0, first_scen
                       F=np.ascontiguousarray(F), pairs=np.asarray(pairs, np.int32),
                       n_scenes=n_scenes, n_cams=n_cams, seed=seed,
                       meta={"first_scene": first_scene, "n_dets": n_dets, "ragged": ragged})
+
+
+@dataclass
+class DetectorBatch:
+    """Synthetic detector outputs of S 3-camera captures (what YOLO's
+    ``results.boxes`` would hold), image 3s + c = capture s, camera c.
+
+    boxes  f32 [n, 4] xyxy with fractional parts (int() truncates them)
+    conf   f32 [n]    true detections >= 0.2; clutter partly below threshold
+    cls    f32 [n]    0 for the object, 1 for some clutter
+    img_offs i64 [3S + 1]
+    Ks f32 [S, 3, 3, 3], RTs f64 [S, 3, 4, 4]
+    """
+    boxes: np.ndarray
+    conf: np.ndarray
+    cls: np.ndarray
+    img_offs: np.ndarray
+    Ks: np.ndarray
+    RTs: np.ndarray
+
+    @property
+    def n_captures(self) -> int:
+        return int(self.Ks.shape[0])
+
+
+def make_detector_batch(n_captures: int, n_dets: int, *, seed: int = 0, clutter: int = 4,
+                        first_capture: int = 0) -> DetectorBatch:
+    """Per capture ``rng = default_rng(seed + first_capture + s)``: an IPD-like
+    rig, ``n_dets`` boxes per view from ``_views`` (half true objects, half
+    clutter) with sub-pixel offsets, plus up to ``clutter`` detector boxes per
+    view that the conf/class filter of _detect (process_pose.py:130) drops."""
+    boxes, conf, cls, counts = [], [], [], []
+    Ks_all = np.empty((n_captures, 3, 3, 3), np.float32)
+    RTs_all = np.empty((n_captures, 3, 4, 4), np.float64)
+    for s in range(n_captures):
+        rng = np.random.default_rng(seed + first_capture + s)
+        Ks, RTs = make_rig(rng, 3)
+        Ks_all[s], RTs_all[s] = np.stack(Ks), np.stack(RTs)
+        for b, _ in _views(rng, Ks, RTs, [n_dets] * 3, box_px=80.0, noise_px=1.5):
+            b = np.asarray(b, np.float64).reshape(-1, 4)
+            b = b + np.where(b >= 0, 1.0, -1.0) * rng.uniform(0.0, 0.999, b.shape)
+            nj = int(rng.integers(0, clutter + 1))
+            jb = rng.uniform(0.0, IMAGE_SIZE, (nj, 4))
+            jc = np.where(rng.random(nj) < 0.5, rng.uniform(0.0, 0.09, nj), 0.9)
+            jk = np.where(jc > 0.5, 1.0, 0.0)
+            per = rng.permutation(len(b) + nj)
+            boxes.append(np.concatenate([b, jb])[per])
+            conf.append(np.concatenate([rng.uniform(0.2, 1.0, len(b)), jc])[per])
+            cls.append(np.concatenate([np.zeros(len(b)), jk])[per])
+            counts.append(len(b) + nj)
+    img_offs = np.zeros(3 * n_captures + 1, np.int64)
+    np.cumsum(counts, out=img_offs[1:])
+    cat = lambda xs, w: (np.concatenate(xs) if xs else np.zeros((0,) + w))
+    return DetectorBatch(boxes=np.ascontiguousarray(cat(boxes, (4,)), np.float32).reshape(-1, 4),
+                         conf=np.ascontiguousarray(cat(conf, ()), np.float32),
+                         cls=np.ascontiguousarray(cat(cls, ()), np.float32),
+                         img_offs=img_offs, Ks=Ks_all, RTs=RTs_all)

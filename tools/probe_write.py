@@ -1,0 +1,31 @@
+"""HBM write-probe variants (MVM_PROBE_MODE / MVM_PROBE_GRID), 4 GiB buffer, HIP events."""
+import os, sys, subprocess, json
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+def one():
+    import torch
+    from bpc_baseline_amd import ops
+    buf = torch.empty(1 << 30, dtype=torch.float32, device="cuda")
+    for _ in range(3):
+        ops.hbm_write_probe(buf)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        ops.hbm_write_probe(buf)
+    e1.record()
+    torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / 10 * 1e-3
+    print(json.dumps({"mode": os.environ.get("MVM_PROBE_MODE", "0"), "grid": os.environ.get("MVM_PROBE_GRID", ""),
+                      "TB/s": buf.numel() * 4 / t / 1e12}))
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "one":
+        one()
+    else:
+        for mode, grid in [(0, ""), (1, ""), (2, ""), (3, ""), (4, "1024"), (4, "2048"), (4, "4096"),
+                           (5, "2048"), (5, "4096")]:
+            env = dict(os.environ, MVM_PROBE_MODE=str(mode))
+            if grid:
+                env["MVM_PROBE_GRID"] = grid
+            subprocess.run([sys.executable, __file__, "one"], env=env, check=True, timeout=120)
