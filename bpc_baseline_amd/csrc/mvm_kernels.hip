@@ -927,6 +927,117 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
     }
 }
 
+// ------------------------------------------------- small-scene cube ----
+// Scenes whose views hold at most kSmallMaxN detections (the IPD regime: a
+// few to a few dozen objects per image) are too small for the tiled kernel's
+// 16 x 32 tiles and its fp64 workspace pass.  One workgroup owns one scene:
+// it stages the three views' centroids, the six line sets and the three fp64
+// pair matrices e12 [N][M], e13 [N][P], e23 [M][P] in LDS (exactly the
+// residuals of row_safe: sentinel, 0.5 * (d1 + d2)), then streams the cube in
+// flattened order -- every wave instruction writes 256 contiguous bytes
+// whatever P is -- and finally one thread per (i, j) row recomputes the row's
+// values from LDS for the argmin over k.
+constexpr int kSmallMaxN = 64;
+
+struct CubeSmallArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;            // [S*3, 9]: F12, F13, F23
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t max_n;
+};
+
+__device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
+    const double sum = (e12 + e13) + e23;
+    const double q0 = sum * kThird;
+    return (float)(third_fast_ok(q0) ? q0 : sum / 3.0);
+}
+
+__global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int nmax = args.max_n;
+    double *sp = reinterpret_cast<double *>(s_dyn);         // [3][nmax][2] centroids
+    double *sl = sp + 6 * nmax;                              // [3 pairs][2 sides][nmax][3] lines
+    double *se = sl + 18 * nmax;                             // e12 | e13 | e23, nmax*nmax each
+    unsigned char *sdeg = reinterpret_cast<unsigned char *>(se + 3 * nmax * nmax);  // [3][2][nmax]
+
+    const int s = blockIdx.x, t = threadIdx.x;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t o0 = co[0];
+    const int n[3] = {(int)(co[1] - co[0]), (int)(co[2] - co[1]), (int)(co[3] - co[2])};
+    const int N = n[0], M = n[1], P = n[2];
+    const int64_t roff = args.row_offs[s];
+    if (N == 0 || M == 0) return;                            // no (i, j) rows, empty cube
+
+    for (int v = 0; v < 3; ++v) {
+        const int64_t ov = co[v] - o0;
+        for (int q = t; q < 2 * n[v]; q += kThreads) sp[(v * nmax) * 2 + q] = args.pts[2 * (o0 + ov) + q];
+    }
+    __syncthreads();
+    // pair p = (a, b): row lines of view a with F_p, column lines of view b
+    const int pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
+    for (int w = t; w < 6 * nmax; w += kThreads) {
+        const int p = w / (2 * nmax), side = (w / nmax) & 1, i = w % nmax;
+        const int v = side ? pb[p] : pa[p];
+        if (i >= n[v]) continue;
+        double f[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) f[q] = args.F[(3 * (int64_t)s + p) * 9 + q];
+        const double x = sp[(v * nmax + i) * 2], y = sp[(v * nmax + i) * 2 + 1];
+        double l0, l1, l2;
+        const bool deg = side ? col_line(f, x, y, l0, l1, l2) : row_line(f, x, y, l0, l1, l2);
+        double *L = sl + ((p * 2 + side) * nmax + i) * 3;
+        L[0] = l0;
+        L[1] = l1;
+        L[2] = l2;
+        sdeg[(p * 2 + side) * nmax + i] = deg;
+    }
+    __syncthreads();
+    for (int p = 0; p < 3; ++p) {
+        const int na = n[pa[p]], nb = n[pb[p]];
+        double *E = se + p * nmax * nmax;
+        for (int w = t; w < na * nb; w += kThreads) {
+            const int i = w / nb, j = w - i * nb;
+            const double *R = sl + ((p * 2 + 0) * nmax + i) * 3;
+            const double *C = sl + ((p * 2 + 1) * nmax + j) * 3;
+            const double rx = sp[(pa[p] * nmax + i) * 2], ry = sp[(pa[p] * nmax + i) * 2 + 1];
+            const double cx = sp[(pb[p] * nmax + j) * 2], cy = sp[(pb[p] * nmax + j) * 2 + 1];
+            const double d1 = sdeg[(p * 2 + 1) * nmax + j] ? kSentinel : line_dist(C[0], C[1], C[2], rx, ry);
+            const double d2 = sdeg[(p * 2 + 0) * nmax + i] ? kSentinel : line_dist(R[0], R[1], R[2], cx, cy);
+            E[i * nb + j] = 0.5 * (d1 + d2);                                          // :28
+        }
+    }
+    __syncthreads();
+    const double *e12 = se, *e13 = se + nmax * nmax, *e23 = se + 2 * nmax * nmax;
+    if (args.cube && P > 0) {
+        float *cb = args.cube + args.cube_offs[s];
+        const int MP = M * P, total = N * MP;
+        for (int f = t; f < total; f += kThreads) {
+            const int i = f / MP, r = f - i * MP, j = r / P, k = r - j * P;
+            __builtin_nontemporal_store(cube_f32(e12[i * M + j], e13[i * P + k], e23[j * P + k]), cb + f);
+        }
+    }
+    for (int w = t; w < N * M; w += kThreads) {
+        const int i = w / M, j = w - i * M;
+        uint32_t bk = kKeyInvalid;
+        int32_t bi = -1;
+        const double a = e12[i * M + j];
+        for (int k = 0; k < P; ++k) {
+            const uint32_t key = key_of(cube_f32(a, e13[i * P + k], e23[j * P + k]));
+            if (key < bk) {
+                bk = key;
+                bi = k;
+            }
+        }
+        if (args.argmin) args.argmin[roff + w] = bi;
+        if (args.minval) args.minval[roff + w] = value_of_key(bk);
+    }
+}
+
 // ------------------------------------------------------- write probe ----
 // Speed-of-light reference for the roofline: every workgroup writes one
 // contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
@@ -1217,6 +1328,27 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     if (((uintptr_t)workspace_dev & 15) != 0)
         return fail(MVM_ERR_INVALID_ARGUMENT, "workspace not 16-byte aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled, 2 register, 1 generic
+    if (max_n <= kSmallMaxN && env_int("MVM_TRIPLET_SMALL", 1) && variant == 3) {
+        // one workgroup per scene, everything in LDS, no workspace pass
+        CubeSmallArgs c{};
+        c.pts = pts_dev;
+        c.cam_offs = cam_offs_dev;
+        c.F = F_dev;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.max_n = max_n;
+        const size_t lds = (size_t)max_n * (24 + 3 * (size_t)max_n) * sizeof(double) + 6 * (size_t)max_n;
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute(reinterpret_cast<const void *>(&triplet_small_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+        triplet_small_kernel<<<dim3((unsigned)n_scenes), dim3(kThreads), lds, s>>>(c);
+        return check_launch("triplet_small_kernel");
+    }
     const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;
     const int64_t mat_stride = (int64_t)max_n * ld;
     // pairs (0,1), (0,2), (1,2): F12, F13, F23 (process_pose.py:157-159)
@@ -1224,7 +1356,6 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     int st = mvm_pairwise_residual_f64(pts_dev, cam_offs_dev, F_dev, pa, pb, n_scenes, 3, 3,
                                        max_n, mat_stride, ld, (double *)workspace_dev, stream);
     if (st) return st;
-    const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled, 2 register, 1 generic
     if (max_n <= kChunk && variant == 3) {
         // tile shape knob MVM_TRIPLET_TILE: 3 = 16i x 32j (default, fastest on
         // MI355X), 0 = 16i x 16j, 1 = 8i x 16j, 2 = 8i x 32j

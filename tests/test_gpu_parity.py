@@ -136,10 +136,21 @@ def test_pairwise_argmin_only(cuda):
 
 
 # --------------------------------------------------------------- cube ----
-def test_cube_golden_batched(cuda, golden):
+@pytest.fixture(params=["small", "tiled"])
+def cube_path(request, monkeypatch):
+    """Run a cube test through the one-workgroup-per-scene kernel (views of
+    <= 64 detections) and through the tiled kernel + fp64 workspace."""
+    monkeypatch.setenv("MVM_TRIPLET_SMALL", "1" if request.param == "small" else "0")
+    return request.param
+
+
+def test_cube_golden_batched(cuda, golden, cube_path):
     """All reference compute_cost_matrix cubes in ONE ragged batched launch."""
     g = golden("a3_cost_cubes.npz")
     names = list(g["names"])
+    if cube_path == "small":      # keep the batch inside the small kernel's range
+        names = [n for n in names if max(len(g[f"{n}_p{v}"]) for v in (1, 2, 3)) <= 64]
+        assert len(names) >= 8
     views, Fs = [], []
     for n in names:
         views += [g[f"{n}_p1"], g[f"{n}_p2"], g[f"{n}_p3"]]
@@ -158,8 +169,9 @@ def test_cube_golden_batched(cuda, golden):
         ro += N * M
 
 
-@pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False)])
-def test_cube_synthetic_vs_oracle(cuda, S, n, ragged):
+@pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False),
+                                        (300, 24, False), (40, 64, True), (7, 1, False)])
+def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
     c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S)
