@@ -1109,6 +1109,9 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 //   MVM_TRIPLET_RPW / MVM_TRIPLET_GENERIC  cube kernel variant
 //   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
+//   MVM_PAIRWISE_NT   1: nontemporal row stores (default), 0: default policy
+//   MVM_TRIPLET_SMALL 1: one-workgroup-per-scene cube for views of <= 64
+//   MVM_LSAP_WAVE_MAX_COLS  long-side limit of the one-wave LSAP (mvm_lsap.hip)
 int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
     return e ? atoi(e) : dflt;
@@ -1190,6 +1193,8 @@ int mvm_fail(int code, const char *fmt, ...) {
     va_end(ap);
     return code;
 }
+
+int mvm_env_int(const char *name, int dflt) { return env_int(name, dflt); }
 
 int mvm_check_launch(const char *what) {
     const hipError_t err = hipGetLastError();

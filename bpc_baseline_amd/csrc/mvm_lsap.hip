@@ -49,6 +49,7 @@ struct LsapArgs {
     int64_t *row_ind;
     int64_t *col_ind;
     int32_t *status;            // 0 ok, 1 invalid entries (NaN / -inf), 2 infeasible
+    int32_t wave_max_cols;      // problems with max(rows, cols) <= this run in lsap_wave_kernel
 };
 
 struct Red {
@@ -121,6 +122,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
         if (t == 0) a.status[p] = 0;
         return;
     }
+    if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const Layout L = lsap_layout(nr, nc, transpose);
@@ -305,6 +307,199 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
     if (t == 0) a.status[p] = 0;
 }
 
+// ------------------------------------------------ one wave per problem ----
+// Problems whose long side fits 64 * kWaveMaxK columns (every scene of a few
+// dozen detections: (N*M) x P = 576 x 24 at 24 per view) are solved by ONE
+// wave with no workgroup barriers: lane l keeps the per-column state of
+// columns l, l + 64, ... in registers (spc, v, path, row4col, scan
+// position, SC flag), the row duals u and col4row sit in the wave's LDS slice,
+// and every decision is a wave-wide reduction.  Same algorithm and tie rule
+// as lsap_kernel (and scipy): the row dual update is driven from the columns
+// -- a visited row i != cur is row4col[j] of exactly one visited column j, and
+// col4row[i] == j -- so no SR list is needed.
+constexpr int kWaveMaxK = 16;              // columns per lane -> long side <= 1024
+constexpr int kWaveProblems = 4;           // waves (problems) per workgroup
+constexpr int kWaveMaxCols = 64 * kWaveMaxK;
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int K>
+__device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_t R, int64_t Kc, double *u,
+                                int32_t *c4r, int lane) {
+    const bool transpose = Kc < R;
+    const int nr = (int)(transpose ? Kc : R), nc = (int)(transpose ? R : Kc);
+    const Layout L = lsap_layout(nr, nc, transpose);
+    unsigned char *w = a.ws + a.ws_offs[p];
+    const float *C0 = a.cost + a.cost_offs[p];
+    const float *Ct = transpose ? reinterpret_cast<const float *>(w + L.ct) : C0;
+
+    // validate (NaN / -inf, as scipy) and transpose a tall matrix
+    int bad = 0;
+    if (transpose) {
+        float *Ctw = reinterpret_cast<float *>(w + L.ct);   // [nr][nc] = C0^T
+        for (int64_t x = lane; x < R * Kc; x += 64) {
+            const float val = C0[x];
+            bad |= (val != val) || (val == -INFINITY);
+            const int64_t j = x / Kc, i = x - j * Kc;
+            Ctw[i * nc + j] = val;
+        }
+    } else {
+        for (int64_t x = lane; x < R * Kc; x += 64) {
+            const float val = C0[x];
+            bad |= (val != val) || (val == -INFINITY);
+        }
+    }
+    if (__ballot(bad)) {
+        if (lane == 0) a.status[p] = 1;
+        return;
+    }
+    for (int i = lane; i < nr; i += 64) {
+        u[i] = 0.0;
+        c4r[i] = -1;
+    }
+    double spc[K], v[K];
+    int32_t path[K], r4c[K], pos[K];
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        v[q] = 0.0;
+        path[q] = -1;
+        r4c[q] = -1;
+    }
+    wave_sync();
+
+    for (int cur = 0; cur < nr; ++cur) {
+        uint32_t insc = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const int j = lane + 64 * q;
+            spc[q] = INFINITY;
+            pos[q] = j < nc ? nc - 1 - j : -1;   // scan array starts in reverse column order
+        }
+        int i = cur, nrem = nc, sink = -1;
+        double min_val = 0.0;
+        while (sink < 0) {
+            const double ui = u[i];
+            const float *Ci = Ct + (int64_t)i * nc;
+            Red best{INFINITY, 0x7FFFFFFF, -1};
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                if (pos[q] < 0) continue;
+                const double r = ((min_val + (double)Ci[lane + 64 * q]) - ui) - v[q];
+                if (r < spc[q]) {
+                    path[q] = i;
+                    spc[q] = r;
+                }
+                const double sj = spc[q];
+                const bool free_col = r4c[q] == -1;
+                if (sj < best.m) {
+                    best.m = sj;
+                    best.first = pos[q];
+                    best.last_free = free_col ? pos[q] : -1;
+                } else if (sj == best.m) {
+                    best.first = min(best.first, pos[q]);
+                    if (free_col) best.last_free = max(best.last_free, pos[q]);
+                }
+            }
+            best = red_wave(best);
+            if (!(best.m < INFINITY)) {
+                if (lane == 0) a.status[p] = 2;   // infeasible
+                return;
+            }
+            const int index = best.last_free >= 0 ? best.last_free : best.first;
+            --nrem;
+            // the chosen column (scan position index) and the scan array's last
+            // one, as per-lane slot masks: data-driven selects only, so the
+            // register arrays are never indexed dynamically (no scratch)
+            uint32_t jm = 0, lm = 0;
+            int32_t r4 = -1, jcol = -1;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const bool hit = pos[q] == index;
+                jm |= hit ? 1u << q : 0u;
+                lm |= pos[q] == nrem ? 1u << q : 0u;
+                r4 = hit ? r4c[q] : r4;
+                jcol = hit ? lane + 64 * q : jcol;
+            }
+            const int jl = (int)__builtin_ctzll(__ballot(jm != 0));
+            const int j = __builtin_amdgcn_readlane(jcol, jl);
+            r4 = __builtin_amdgcn_readlane(r4, jl);
+            min_val = best.m;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                if (lm & (1u << q)) pos[q] = index;   // remaining[index] = remaining[nrem]
+                if (jm & (1u << q)) pos[q] = -1;      // (after: last == j leaves j removed)
+            }
+            insc |= jm;
+            if (r4 == -1) sink = j;
+            else i = r4;
+        }
+        // dual updates
+        if (lane == 0) u[cur] += min_val;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            if (insc & (1u << q)) {
+                if (r4c[q] != -1) u[r4c[q]] += min_val - spc[q];
+                v[q] -= min_val - spc[q];
+            }
+        }
+        wave_sync();
+        // augment along the path
+        int j = sink;
+        while (true) {
+            int32_t pj = -1;
+#pragma unroll
+            for (int q = 0; q < K; ++q) pj = (lane + 64 * q == j) ? path[q] : pj;
+            const int i2 = __builtin_amdgcn_readlane(pj, j % 64);
+#pragma unroll
+            for (int q = 0; q < K; ++q) r4c[q] = (lane + 64 * q == j) ? i2 : r4c[q];
+            const int prev = c4r[i2];
+            wave_sync();
+            if (lane == 0) c4r[i2] = j;
+            wave_sync();
+            j = prev;
+            if (i2 == cur) break;
+        }
+    }
+
+    // output pairs in scipy's order
+    const int64_t o = a.out_offs[p];
+    if (transpose) {
+        for (int k = lane; k < nr; k += 64) {
+            const int32_t rk = c4r[k];
+            int rank = 0;
+            for (int k2 = 0; k2 < nr; ++k2) rank += c4r[k2] < rk;
+            a.row_ind[o + rank] = rk;
+            a.col_ind[o + rank] = k;
+        }
+    } else {
+        for (int i = lane; i < nr; i += 64) {
+            a.row_ind[o + i] = i;
+            a.col_ind[o + i] = c4r[i];
+        }
+    }
+    if (lane == 0) a.status[p] = 0;
+}
+
+template <int K>
+__global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs a, int32_t n) {
+    __shared__ double s_u[kWaveProblems][64 * K];      // rows <= long side <= 64 K
+    __shared__ int32_t s_c4r[kWaveProblems][64 * K];
+    const int lane = threadIdx.x % 64;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+    const int p = blockIdx.x * kWaveProblems + wave;
+    if (p >= n) return;
+    const int64_t R = a.dims[2 * p], Kc = a.dims[2 * p + 1];
+    const int64_t nc = R > Kc ? R : Kc;
+    if (R == 0 || Kc == 0 || nc > a.wave_max_cols) return;   // empty: lsap_kernel sets status
+    // each instantiation owns the long sides (32K, 64K]: its own register budget
+    if (nc > 64 * K || (K > 1 && nc <= 32 * K)) return;
+    lsap_wave_solve<K>(a, p, R, Kc, s_u[wave], s_c4r[wave], lane);
+}
+
 }  // namespace
 
 extern "C" {
@@ -345,11 +540,24 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     if (!workspace_dev && workspace_bytes)
         return mvm_fail(MVM_ERR_WORKSPACE, "null workspace");
+    // MVM_LSAP_WAVE_MAX_COLS: long-side limit of the one-wave-per-problem kernel
+    // (0 disables it; capped at 1024)
+    int wave_max = mvm_env_int("MVM_LSAP_WAVE_MAX_COLS", kWaveMaxCols);
+    wave_max = wave_max < 0 ? 0 : (wave_max > kWaveMaxCols ? kWaveMaxCols : wave_max);
     LsapArgs a{cost_dev, cost_offs_dev, dims_dev, ws_offs_dev,
                reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
-               col_ind_dev, status_dev};
-    lsap_kernel<<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0,
-                  reinterpret_cast<hipStream_t>(stream)>>>(a);
+               col_ind_dev, status_dev, wave_max};
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (wave_max > 0) {
+        const dim3 grid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
+        const dim3 block(64 * kWaveProblems);
+        lsap_wave_kernel<1><<<grid, block, 0, s>>>(a, n_problems);
+        if (wave_max > 64) lsap_wave_kernel<2><<<grid, block, 0, s>>>(a, n_problems);
+        if (wave_max > 128) lsap_wave_kernel<4><<<grid, block, 0, s>>>(a, n_problems);
+        if (wave_max > 256) lsap_wave_kernel<8><<<grid, block, 0, s>>>(a, n_problems);
+        if (wave_max > 512) lsap_wave_kernel<16><<<grid, block, 0, s>>>(a, n_problems);
+    }
+    lsap_kernel<<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");
 }
 

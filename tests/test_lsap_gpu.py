@@ -22,10 +22,19 @@ def _batched(cuda, mats):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-def test_random_shapes_and_ties_batched(cuda):
+@pytest.fixture(params=["wave", "workgroup"])
+def lsap_path(request, monkeypatch):
+    """Problems with a long side <= 1024 run one per wave by default; the
+    workgroup kernel solves the rest (and everything when the knob is 0)."""
+    monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "1024" if request.param == "wave" else "0")
+    return request.param
+
+
+def test_random_shapes_and_ties_batched(cuda, lsap_path):
     rng = np.random.default_rng(0)
     mats = []
-    for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0)]:
+    for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0),
+                  (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70)]:
         for trial in range(4):
             c = rng.normal(size=shape).astype(np.float32)
             if trial == 1:
@@ -41,7 +50,7 @@ def test_random_shapes_and_ties_batched(cuda):
         assert np.array_equal(r, r0) and np.array_equal(c, c0), m.shape
 
 
-def test_golden_match_lists(cuda, golden):
+def test_golden_match_lists(cuda, golden, lsap_path):
     from bpc_baseline_amd.inference.epipolar_matching import match_objects
     g = golden("a3_cost_cubes.npz")
     for n in g["names"]:
@@ -51,7 +60,7 @@ def test_golden_match_lists(cuda, golden):
             assert np.array_equal(got, g[f"{n}_{key}"]), (n, thr)
 
 
-def test_error_statuses(cuda):
+def test_error_statuses(cuda, lsap_path):
     from bpc_baseline_amd.inference.epipolar_matching import linear_sum_assignment
     with pytest.raises(ValueError, match="invalid numeric"):
         linear_sum_assignment(np.array([[np.nan, 1.0], [0.0, 2.0]]))
