@@ -73,7 +73,7 @@ class MatchBatch:
 def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                    img_offs: torch.Tensor, Ks: np.ndarray, RTs: np.ndarray, *,
                    conf_thresh: float = 0.1, matching_threshold: float = 30,
-                   keep_cube: bool = False) -> MatchBatch:
+                   keep_cube: bool = False, timings: Optional[dict] = None) -> MatchBatch:
     """Detect-packing + matching + triangulation of S 3-camera captures.
 
     ``boxes`` f32 [n, 4] xyxy, ``conf``/``cls`` f32 [n]: the detector outputs
@@ -83,6 +83,16 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     (process_pose.py:36-37).
     """
     dev = boxes.device
+    import time
+    clock = [time.perf_counter()]
+
+    def mark(name):                      # optional stage timings (synchronising)
+        if timings is not None:
+            torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            timings[name] = timings.get(name, 0.0) + now - clock[0]
+            clock[0] = now
+
     n_img = int(img_offs.numel()) - 1
     if n_img % 3:
         raise ValueError("img_offs must describe 3 images per capture")
@@ -92,30 +102,40 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
 
     pts, cam_offs, boxes_int, counts, status = ops.pack_detections(boxes, conf, cls, img_offs,
                                                                    conf_thresh)
+    mark("pack")
     # host work while the packing runs: F and P for every capture
     F = fundamental_matrices_batched(Ks, RTs, camera_pairs(3))
     F_dev = torch.from_numpy(F.reshape(-1)).to(dev, non_blocking=False)
     proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev)
+    mark("F+P host")
 
     counts_host = counts.cpu().numpy().astype(np.int64)
     if int(status.item()) != 0:
         raise ValueError("detector box with a non-finite or out-of-range coordinate")
     cam_offs_host = np.zeros(n_img + 1, np.int64)
     np.cumsum(counts_host, out=cam_offs_host[1:])
+    mark("counts D2H")
 
     plan = ops.TripletPlan(cam_offs_host, S, device=dev)
+    mark("cube plan")
     cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan)
+    mark("cube")
     c3 = counts_host.reshape(S, 3)
     lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+    mark("lsap plan")
     row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(cube, plan.cube_offs[:-1].contiguous(),
                                                                 lplan)
+    mark("lsap")
     match, cost, X, count = ops.select_triangulate(cube, plan.cube_offs, cam_offs, lplan.out_offs,
                                                    row_ind, col_ind, pts, proj_dev,
                                                    float(matching_threshold))
+    mark("select")
     bad = lstat.cpu().numpy()
     if np.any(bad):
         raise ValueError(f"assignment failed for captures {np.nonzero(bad)[0][:8].tolist()} "
                          "(cost matrix contains invalid numeric entries or is infeasible)")
-    return MatchBatch(match=match, cost=cost, X=X, count=count.cpu().numpy(),
+    count_h = count.cpu().numpy()
+    mark("results D2H")
+    return MatchBatch(match=match, cost=cost, X=X, count=count_h,
                       offs=lplan.out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
                       cube=cube if keep_cube else None)

@@ -121,8 +121,8 @@ def fundamental_matrices_batched(Ks: np.ndarray, RTs: np.ndarray, pairs: np.ndar
     skew[..., 1, 0], skew[..., 1, 2] = t_rel[..., 2], -t_rel[..., 0]
     skew[..., 2, 0], skew[..., 2, 1] = -t_rel[..., 1], t_rel[..., 0]
     essential = skew @ R_rel
-    K1inv = np.linalg.inv(Ks[:, a])
-    K2inv = np.linalg.inv(Ks[:, b])
+    Kinv = np.linalg.inv(Ks)             # once per camera; each matrix solved on its own
+    K1inv, K2inv = Kinv[:, a], Kinv[:, b]
     F = np.swapaxes(K2inv, -1, -2) @ essential @ K1inv
     f22 = F[..., 2:3, 2:3]
     F = np.where(np.abs(f22) > 1e-8, F / np.where(np.abs(f22) > 1e-8, f22, 1.0), F)

@@ -61,6 +61,10 @@ def main():
         res = match_captures(boxes, conf, cls, offs, b.Ks, b.RTs)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
+    stages = {}
+    for _ in range(args.steps):
+        match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, timings=stages)
+    stages = {k: round(v / args.steps * 1e3, 3) for k, v in stages.items()}
 
     # parity spot-check on a few captures, then the CPU chain on a sample
     rng = np.random.default_rng(0)
@@ -82,6 +86,7 @@ def main():
         "value": args.captures / dt, "unit": "captures/s", "ms_per_batch": dt * 1e3,
         "config": {"captures": args.captures, "dets_per_view": args.dets, "cams": 3},
         "matches": int(res.count.sum()), "parity_checked": len(check),
+        "stage_ms_synchronised": stages,
         "cpu_chain": {"value": cpu, "unit": "captures/s", "cores": 1, "kind": "port",
                       "sample": f"first {k} captures, oracle C cube + scipy LSA + numpy SVD"},
     }))
