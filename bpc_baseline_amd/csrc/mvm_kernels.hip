@@ -930,13 +930,14 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
 // ------------------------------------------------- small-scene cube ----
 // Scenes whose views hold at most kSmallMaxN detections (the IPD regime: a
 // few to a few dozen objects per image) are too small for the tiled kernel's
-// 16 x 32 tiles and its fp64 workspace pass.  One workgroup owns one scene:
-// it stages the three views' centroids, the six line sets and the three fp64
-// pair matrices e12 [N][M], e13 [N][P], e23 [M][P] in LDS (exactly the
-// residuals of row_safe: sentinel, 0.5 * (d1 + d2)), then streams the cube in
-// flattened order -- every wave instruction writes 256 contiguous bytes
-// whatever P is -- and finally one thread per (i, j) row recomputes the row's
-// values from LDS for the argmin over k.
+// 16 x 32 tiles and its fp64 workspace pass.  A workgroup owns (scene, block
+// of `ib` rows i): it stages the three views' centroids, the six line sets,
+// e23 [M][P] and its rows of e12 [ib][M], e13 [ib][P] in LDS (exactly the
+// residuals of row_safe: sentinel, 0.5 * (d1 + d2)), then streams its
+// contiguous slice of the cube in flattened order -- 16-byte nontemporal
+// stores, indices advanced incrementally (no divisions in the loop), every
+// wave instruction 1 KiB contiguous whatever P is -- and finally one thread
+// per (i, j) row recomputes the row from LDS for the argmin over k.
 constexpr int kSmallMaxN = 64;
 
 struct CubeSmallArgs {
@@ -949,7 +950,14 @@ struct CubeSmallArgs {
     int32_t *argmin;
     float *minval;
     int32_t max_n;
+    int32_t ib;                 // rows i per workgroup
+    int32_t i_blocks;           // ceil(max_n / ib)
 };
+
+__host__ __device__ inline size_t small_lds_bytes(int nmax, int ib) {
+    return ((size_t)24 * nmax + 2 * (size_t)ib * nmax + (size_t)nmax * nmax) * sizeof(double) +
+           6 * (size_t)nmax;
+}
 
 __device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
     const double sum = (e12 + e13) + e23;
@@ -959,19 +967,23 @@ __device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
 
 __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-    const int nmax = args.max_n;
+    const int nmax = args.max_n, IB = args.ib;
     double *sp = reinterpret_cast<double *>(s_dyn);         // [3][nmax][2] centroids
     double *sl = sp + 6 * nmax;                              // [3 pairs][2 sides][nmax][3] lines
-    double *se = sl + 18 * nmax;                             // e12 | e13 | e23, nmax*nmax each
-    unsigned char *sdeg = reinterpret_cast<unsigned char *>(se + 3 * nmax * nmax);  // [3][2][nmax]
+    double *s12 = sl + 18 * nmax;                            // [ib][M]
+    double *s13 = s12 + IB * nmax;                           // [ib][P]
+    double *s23 = s13 + IB * nmax;                           // [M][P]
+    unsigned char *sdeg = reinterpret_cast<unsigned char *>(s23 + nmax * nmax);  // [3][2][nmax]
 
-    const int s = blockIdx.x, t = threadIdx.x;
+    const int s = blockIdx.x / args.i_blocks, t = threadIdx.x;
+    const int i0 = (blockIdx.x - s * args.i_blocks) * IB;
     const int64_t *co = args.cam_offs + 3 * (int64_t)s;
     const int64_t o0 = co[0];
     const int n[3] = {(int)(co[1] - co[0]), (int)(co[2] - co[1]), (int)(co[3] - co[2])};
     const int N = n[0], M = n[1], P = n[2];
+    if (i0 >= N || M == 0) return;                           // no (i, j) rows in this block
+    const int nb = min(IB, N - i0);
     const int64_t roff = args.row_offs[s];
-    if (N == 0 || M == 0) return;                            // no (i, j) rows, empty cube
 
     for (int v = 0; v < 3; ++v) {
         const int64_t ov = co[v] - o0;
@@ -997,44 +1009,88 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
         sdeg[(p * 2 + side) * nmax + i] = deg;
     }
     __syncthreads();
+    // e_ab(i, j) of row_safe: pairs (0,1) and (0,2) for this block's rows, (1,2) whole
+    const int rows_of[3] = {nb, nb, M}, first_of[3] = {i0, i0, 0};
+    double *dst_of[3] = {s12, s13, s23};
     for (int p = 0; p < 3; ++p) {
-        const int na = n[pa[p]], nb = n[pb[p]];
-        double *E = se + p * nmax * nmax;
-        for (int w = t; w < na * nb; w += kThreads) {
-            const int i = w / nb, j = w - i * nb;
+        const int na = rows_of[p], nbb = n[pb[p]], r0 = first_of[p];
+        double *E = dst_of[p];
+        for (int w = t; w < na * nbb; w += kThreads) {
+            const int il = w / nbb, j = w - il * nbb, i = r0 + il;
             const double *R = sl + ((p * 2 + 0) * nmax + i) * 3;
             const double *C = sl + ((p * 2 + 1) * nmax + j) * 3;
             const double rx = sp[(pa[p] * nmax + i) * 2], ry = sp[(pa[p] * nmax + i) * 2 + 1];
             const double cx = sp[(pb[p] * nmax + j) * 2], cy = sp[(pb[p] * nmax + j) * 2 + 1];
             const double d1 = sdeg[(p * 2 + 1) * nmax + j] ? kSentinel : line_dist(C[0], C[1], C[2], rx, ry);
             const double d2 = sdeg[(p * 2 + 0) * nmax + i] ? kSentinel : line_dist(R[0], R[1], R[2], cx, cy);
-            E[i * nb + j] = 0.5 * (d1 + d2);                                          // :28
+            E[w] = 0.5 * (d1 + d2);                                                   // :28
         }
     }
     __syncthreads();
-    const double *e12 = se, *e13 = se + nmax * nmax, *e23 = se + 2 * nmax * nmax;
+
     if (args.cube && P > 0) {
-        float *cb = args.cube + args.cube_offs[s];
-        const int MP = M * P, total = N * MP;
-        for (int f = t; f < total; f += kThreads) {
-            const int i = f / MP, r = f - i * MP, j = r / P, k = r - j * P;
-            __builtin_nontemporal_store(cube_f32(e12[i * M + j], e13[i * P + k], e23[j * P + k]), cb + f);
+        const int MP = M * P, total = nb * MP;
+        const int64_t gbase = args.cube_offs[s] + (int64_t)i0 * MP;
+        float *cb = args.cube + gbase;
+        const int head = min(total, (int)((4 - (gbase & 3)) & 3));   // to a 16-byte boundary
+        const int body = (total - head) / 4;                          // float4 groups
+        if (t < head) {
+            const int il = t / MP, r = t - il * MP, j = r / P, k = r - j * P;
+            __builtin_nontemporal_store(cube_f32(s12[il * M + j], s13[il * P + k], s23[j * P + k]), cb + t);
+        }
+        const int tail0 = head + 4 * body;
+        if (t < total - tail0) {
+            const int f = tail0 + t;
+            const int il = f / MP, r = f - il * MP, j = r / P, k = r - j * P;
+            __builtin_nontemporal_store(cube_f32(s12[il * M + j], s13[il * P + k], s23[j * P + k]), cb + f);
+        }
+        if (t < body) {
+            // element f = head + 4g for group g = t + 256 * iter; advance by 1024 elements
+            int f = head + 4 * t;
+            int il = f / MP, r = f - il * MP, j = r / P, k = r - j * P;
+            constexpr int kStep = 4 * kThreads;
+            const int dk = kStep % P, q = kStep / P, dj = q % M, dil = q / M;
+            for (int g = t; g < body; g += kThreads) {
+                float v4[4];
+                int a = il, b = j, c = k;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v4[e] = cube_f32(s12[a * M + b], s13[a * P + c], s23[b * P + c]);
+                    if (++c == P) {
+                        c = 0;
+                        if (++b == M) {
+                            b = 0;
+                            ++a;
+                        }
+                    }
+                }
+                const f32x4 vv = {v4[0], v4[1], v4[2], v4[3]};
+                __builtin_nontemporal_store(vv, reinterpret_cast<f32x4 *>(cb + head) + g);
+                k += dk;
+                const int ck = k >= P;
+                k -= ck ? P : 0;
+                j += dj + ck;
+                const int cj = j >= M;
+                j -= cj ? M : 0;
+                il += dil + cj;
+            }
         }
     }
-    for (int w = t; w < N * M; w += kThreads) {
-        const int i = w / M, j = w - i * M;
+    for (int w = t; w < nb * M; w += kThreads) {
+        const int il = w / M, j = w - il * M;
         uint32_t bk = kKeyInvalid;
         int32_t bi = -1;
-        const double a = e12[i * M + j];
+        const double a = s12[w];
         for (int k = 0; k < P; ++k) {
-            const uint32_t key = key_of(cube_f32(a, e13[i * P + k], e23[j * P + k]));
+            const uint32_t key = key_of(cube_f32(a, s13[il * P + k], s23[j * P + k]));
             if (key < bk) {
                 bk = key;
                 bi = k;
             }
         }
-        if (args.argmin) args.argmin[roff + w] = bi;
-        if (args.minval) args.minval[roff + w] = value_of_key(bk);
+        const int64_t row = roff + (int64_t)i0 * M + w;
+        if (args.argmin) args.argmin[row] = bi;
+        if (args.minval) args.minval[row] = value_of_key(bk);
     }
 }
 
@@ -1346,12 +1402,22 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
         c.argmin = argmin_dev;
         c.minval = minval_dev;
         c.max_n = max_n;
-        const size_t lds = (size_t)max_n * (24 + 3 * (size_t)max_n) * sizeof(double) + 6 * (size_t)max_n;
+        // MVM_TRIPLET_SMALL_IB: rows i per workgroup.  Default: the whole scene up
+        // to 32 detections, then 16-row blocks (measured on MI355X: 1.2-1.6 TB/s
+        // from 16 to 64 detections, 2-10x the tiled path; tools/gpu_cube_small.sh)
+        c.ib = env_int("MVM_TRIPLET_SMALL_IB", max_n <= 32 ? max_n : 16);
+        c.ib = c.ib < 1 ? 1 : (c.ib > max_n ? max_n : c.ib);
+        c.i_blocks = (max_n + c.ib - 1) / c.ib;
+        const size_t lds = small_lds_bytes(max_n, c.ib);
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute(reinterpret_cast<const void *>(&triplet_small_kernel),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
-        triplet_small_kernel<<<dim3((unsigned)n_scenes), dim3(kThreads), lds, s>>>(c);
+        const int64_t blocks = (int64_t)n_scenes * c.i_blocks;
+        if (blocks > 0x7FFFFFFFLL)
+            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+        triplet_small_kernel<<<dim3((unsigned)blocks), dim3(kThreads), lds, s>>>(c);
         return check_launch("triplet_small_kernel");
     }
     const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;

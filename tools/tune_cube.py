@@ -18,7 +18,12 @@ out = (torch.empty(plan.n_cube, dtype=torch.float32, device=dev),
        torch.empty(plan.n_rows, dtype=torch.int32, device=dev),
        torch.empty(plan.n_rows, dtype=torch.float32, device=dev))
 nbytes = 4.0 * plan.n_cube + 8.0 * plan.n_rows + 16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0]
-env = {"tile": {"MVM_TRIPLET_VARIANT": "3"},
+env = {"tile": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0"},
+       "small": {"MVM_TRIPLET_SMALL": "1"},
+       "small4": {"MVM_TRIPLET_SMALL": "1", "MVM_TRIPLET_SMALL_IB": "4"},
+       "small8": {"MVM_TRIPLET_SMALL": "1", "MVM_TRIPLET_SMALL_IB": "8"},
+       "small32": {"MVM_TRIPLET_SMALL": "1", "MVM_TRIPLET_SMALL_IB": "32"},
+       "small64": {"MVM_TRIPLET_SMALL": "1", "MVM_TRIPLET_SMALL_IB": "64"},
        "t16x16": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "0"},
        "t8x16": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "1"},
        "t8x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "2"},
@@ -30,7 +35,8 @@ times = {v: [] for v in args.variants.split(",")}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in times:
-        for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_VARIANT", "MVM_TRIPLET_TILE"):
+        for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_VARIANT", "MVM_TRIPLET_TILE", "MVM_TRIPLET_SMALL",
+                  "MVM_TRIPLET_SMALL_IB"):
             os.environ.pop(k, None)
         os.environ.update(env[v])
         ops.triplet_cost_argmin(pts, co, F, plan, out=out)
