@@ -169,14 +169,21 @@ typedef f32x4 __attribute__((address_space(1))) g_f32x4;   // global (AS 1) poin
 // Row store from a scalar (SGPR) row address + a 32-bit per-lane byte offset:
 // lowers to `global_store_dwordx4 v_off, v_data, s_base nt` (saddr form, no
 // per-row 64-bit VALU address arithmetic).
-template <bool NT = true>
+// Store policy POL: 1 nt (default of the residual kernels), 0 default policy,
+// 2 sc1, 3 sc0 sc1 (the last two through inline asm: no builtin exposes them;
+// they drop the line from the XCD's L2 instead of keeping it)
+template <int POL = 1>
 __device__ __forceinline__ void store4_nt_row(uint64_t row_base, uint32_t byte_off,
                                               const float v4[4]) {
     const f32x4 v = {v4[0], v4[1], v4[2], v4[3]};
-    if constexpr (NT)
+    if constexpr (POL == 1)
         __builtin_nontemporal_store(v, reinterpret_cast<g_f32x4 *>(row_base + byte_off));
-    else
+    else if constexpr (POL == 0)
         *reinterpret_cast<g_f32x4 *>(row_base + byte_off) = v;
+    else if constexpr (POL == 2)
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc1" ::"v"(byte_off), "v"(v), "s"(row_base) : "memory");
+    else
+        asm volatile("global_store_dwordx4 %0, %1, %2 sc0 sc1" ::"v"(byte_off), "v"(v), "s"(row_base) : "memory");
 }
 __device__ __forceinline__ void store4_nt(double *dst, const double e[4]) {
     const f64x2 lo = {e[0], e[1]}, hi = {e[2], e[3]};
@@ -270,7 +277,7 @@ __device__ __forceinline__ uint32_t best_key(const Best &b) {
 
 // One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
 // per pair, one 16-byte store, 3 int ops of argmin per pair.
-template <bool ARGMIN, bool STORE, typename OutT, bool NT = true>
+template <bool ARGMIN, bool STORE, typename OutT, int NT = 1>
 __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, OutT *drow, int jbase, Best &best) {
     double e[kColsPerLane];
@@ -320,7 +327,7 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
-template <int RPW, bool ARGMIN, typename OutT, bool NT = true>
+template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
 __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
@@ -1112,6 +1119,24 @@ __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_
     }
 }
 
+// cache-policy variants of the 16 KiB/WG stream (inline asm: the builtins
+// expose only nt); POL 1 = sc1, 2 = sc0 sc1, 3 = nt sc1
+template <int POL>
+__global__ __launch_bounds__(kThreads) void write_probe_pol_kernel(f32x4 *dst, size_t n16, float val) {
+    const f32x4 v = {val, val, val, val};
+    const size_t base = (size_t)blockIdx.x * (4 * kThreads) + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const size_t i = base + (size_t)k * kThreads;
+        if (i < n16) {
+            const uint64_t ptr = reinterpret_cast<uint64_t>(dst + i);
+            if (POL == 1) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(v) : "memory");
+            if (POL == 2) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(ptr), "v"(v) : "memory");
+            if (POL == 3) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(ptr), "v"(v) : "memory");
+        }
+    }
+}
+
 // grid-stride variant: a fixed grid of `waves per CU` x 256 CUs workgroups
 template <bool NT>
 __global__ __launch_bounds__(kThreads) void write_probe_stride_kernel(f32x4 *dst, size_t n16,
@@ -1165,7 +1190,7 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 //   MVM_TRIPLET_RPW / MVM_TRIPLET_GENERIC  cube kernel variant
 //   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
-//   MVM_PAIRWISE_NT   1: nontemporal row stores (default), 0: default policy
+//   MVM_PAIRWISE_NT   row store policy: 1 nt (default), 0 default, 2 sc1, 3 sc0 sc1
 //   MVM_TRIPLET_SMALL 1: one-workgroup-per-scene cube for views of <= 64
 //   MVM_LSAP_WAVE_MAX_COLS  long-side limit of the one-wave LSAP (mvm_lsap.hip)
 int env_int(const char *name, int dflt) {
@@ -1192,12 +1217,25 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg);
     if (f64) {
         pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
-    } else if (env_int("MVM_PAIRWISE_NT", 1)) {
-        if (argmin) pairwise_kernel<RPW, true, float, true><<<grid, block, lds, stream>>>(a);
-        else pairwise_kernel<RPW, false, float, true><<<grid, block, lds, stream>>>(a);
     } else {
-        if (argmin) pairwise_kernel<RPW, true, float, false><<<grid, block, lds, stream>>>(a);
-        else pairwise_kernel<RPW, false, float, false><<<grid, block, lds, stream>>>(a);
+        switch (env_int("MVM_PAIRWISE_NT", 1)) {
+        case 0:
+            if (argmin) pairwise_kernel<RPW, true, float, 0><<<grid, block, lds, stream>>>(a);
+            else pairwise_kernel<RPW, false, float, 0><<<grid, block, lds, stream>>>(a);
+            break;
+        case 2:
+            if (argmin) pairwise_kernel<RPW, true, float, 2><<<grid, block, lds, stream>>>(a);
+            else pairwise_kernel<RPW, false, float, 2><<<grid, block, lds, stream>>>(a);
+            break;
+        case 3:
+            if (argmin) pairwise_kernel<RPW, true, float, 3><<<grid, block, lds, stream>>>(a);
+            else pairwise_kernel<RPW, false, float, 3><<<grid, block, lds, stream>>>(a);
+            break;
+        default:
+            if (argmin) pairwise_kernel<RPW, true, float, 1><<<grid, block, lds, stream>>>(a);
+            else pairwise_kernel<RPW, false, float, 1><<<grid, block, lds, stream>>>(a);
+            break;
+        }
     }
 }
 
@@ -1346,7 +1384,8 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         return fail(MVM_ERR_INVALID_ARGUMENT, "write probe needs a 16-byte aligned buffer/size");
     const size_t n16 = bytes / 16;
     // MVM_PROBE_MODE (experiments): 0 nt 16 KiB/WG (the residual kernels' form),
-    // 1 plain 16 KiB/WG, 2 nt 64 KiB/WG, 3 plain 64 KiB/WG, 4 nt grid-stride, 5 plain grid-stride
+    // 1 plain 16 KiB/WG, 2 nt 64 KiB/WG, 3 plain 64 KiB/WG, 4 nt grid-stride, 5 plain grid-stride,
+    // 6 sc1, 7 sc0 sc1, 8 nt sc1 (16 KiB/WG)
     const int mode = env_int("MVM_PROBE_MODE", 0);
     const int per = (mode == 2 || mode == 3) ? 16 : 4;
     const size_t blocks = (n16 + per * kThreads - 1) / (per * kThreads);
@@ -1361,6 +1400,9 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         case 3: write_probe_kernel<16, false><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 4: write_probe_stride_kernel<true><<<stride_grid, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 5: write_probe_stride_kernel<false><<<stride_grid, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 6: write_probe_pol_kernel<1><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 7: write_probe_pol_kernel<2><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 8: write_probe_pol_kernel<3><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         default: write_probe_kernel<4, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
     }
     return check_launch("write_probe_kernel");

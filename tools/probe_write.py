@@ -23,9 +23,14 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "one":
         one()
     else:
-        for mode, grid in [(0, ""), (1, ""), (2, ""), (3, ""), (4, "1024"), (4, "2048"), (4, "4096"),
-                           (5, "2048"), (5, "4096")]:
-            env = dict(os.environ, MVM_PROBE_MODE=str(mode))
-            if grid:
-                env["MVM_PROBE_GRID"] = grid
-            subprocess.run([sys.executable, __file__, "one"], env=env, check=True, timeout=120)
+        modes = [(0, ""), (1, ""), (2, ""), (3, ""), (4, "1024"), (4, "2048"), (4, "4096"),
+                 (5, "2048"), (5, "4096"), (6, ""), (7, ""), (8, "")]
+        if len(sys.argv) > 1:
+            keep = set(int(x) for x in sys.argv[1].split(","))
+            modes = [m for m in modes if m[0] in keep]
+        for rep in range(2):
+            for mode, grid in modes:
+                env = dict(os.environ, MVM_PROBE_MODE=str(mode))
+                if grid:
+                    env["MVM_PROBE_GRID"] = grid
+                subprocess.run([sys.executable, __file__, "one"], env=env, check=True, timeout=120)
