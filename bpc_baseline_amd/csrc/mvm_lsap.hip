@@ -50,6 +50,8 @@ struct LsapArgs {
     int64_t *col_ind;
     int32_t *status;            // 0 ok, 1 invalid entries (NaN / -inf), 2 infeasible
     int32_t wave_max_cols;      // problems with max(rows, cols) <= this run in lsap_wave_kernel
+    int32_t multi_g;            // > 1: larger problems run in lsap_multi_kernel, G workgroups each
+    unsigned char *sync;        // per-problem barrier + reduction slots (multi kernel)
 };
 
 struct Red {
@@ -123,6 +125,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
         return;
     }
     if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
+    if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const Layout L = lsap_layout(nr, nc, transpose);
@@ -500,6 +503,325 @@ __global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs 
     lsap_wave_solve<K>(a, p, R, Kc, s_u[wave], s_c4r[wave], lane);
 }
 
+
+// --------------------------------------- G workgroups per problem ----
+// For few large problems (a single 256^3 scene: 65,536 columns) one CU
+// streaming all the column state per Dijkstra step is the bottleneck.  Here G
+// co-resident workgroups (cooperative launch) split the columns; each owns a
+// contiguous range and its state (spc, v, path, pos, and its SC list).  Per
+// step every workgroup scans its range, publishes one reduction record, meets
+// the others at a per-problem barrier, and combines the G records in the same
+// fixed order, so all keep identical copies of the uniform state (current
+// row, minVal, remaining count, sink).  The record also carries what the
+// sequential algorithm would read from other columns: the winner's column
+// and row4col, and the column holding the last scan position (the
+// swap-with-last removal), so pos stays owner-local and no rem array exists.
+// Cross-workgroup data (records, u, path, row4col) is published with
+// agent-scope fences around the barrier.  Barrier waits are bounded: a
+// timeout reports status 3 instead of hanging.
+constexpr int kMultiMaxG = 16;
+constexpr size_t kSyncBytes = 1280;     // counter + flags + 2 x kMultiMaxG records
+
+struct MRed {
+    double m;
+    int32_t first, first_col, first_r4;   // smallest scan position holding m (+ its column, row4col)
+    int32_t last_free, last_free_col;     // largest free scan position holding m (+ column)
+    int32_t last_col;                     // column at scan position nrem - 1 (-1: not here)
+};
+
+__device__ __forceinline__ MRed mred_combine(MRed a, const MRed &b) {
+    const int32_t lc = max(a.last_col, b.last_col);
+    if (b.m < a.m) {
+        a = b;
+    } else if (!(a.m < b.m)) {
+        if (b.first < a.first) {
+            a.first = b.first;
+            a.first_col = b.first_col;
+            a.first_r4 = b.first_r4;
+        }
+        if (b.last_free > a.last_free) {
+            a.last_free = b.last_free;
+            a.last_free_col = b.last_free_col;
+        }
+    }
+    a.last_col = lc;
+    return a;
+}
+
+__device__ __forceinline__ MRed mred_wave(MRed r) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        MRed o;
+        o.m = __shfl_xor(r.m, off, 64);
+        o.first = __shfl_xor(r.first, off, 64);
+        o.first_col = __shfl_xor(r.first_col, off, 64);
+        o.first_r4 = __shfl_xor(r.first_r4, off, 64);
+        o.last_free = __shfl_xor(r.last_free, off, 64);
+        o.last_free_col = __shfl_xor(r.last_free_col, off, 64);
+        o.last_col = __shfl_xor(r.last_col, off, 64);
+        r = mred_combine(r, o);
+    }
+    return r;
+}
+
+struct SyncBlock {
+    unsigned int counter;
+    int flag;          // 1: invalid entries, 2: infeasible, 3: barrier timeout
+    int pad[14];
+    MRed slot[2][kMultiMaxG];
+};
+static_assert(sizeof(SyncBlock) <= kSyncBytes, "sync block too large");
+static_assert(kSyncBytes % 256 == 0, "sync blocks stay 256-byte aligned");
+
+// all G workgroups of a problem; returns false on timeout (flag set to 3)
+__device__ bool group_barrier(SyncBlock *sb, unsigned int target) {
+    __shared__ int s_ok;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();                                   // release this workgroup's writes
+        atomicAdd(&sb->counter, 1u);
+        int ok = 1;
+        for (long spins = 0;; ++spins) {
+            const unsigned int c =
+                __hip_atomic_load(&sb->counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (c >= target) break;
+            if (__hip_atomic_load(&sb->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3 ||
+                spins > (1L << 24)) {
+                atomicExch(&sb->flag, 3);
+                ok = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();                                   // acquire the others' writes
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok;
+}
+
+__global__ __launch_bounds__(kLsapThreads) void lsap_multi_kernel(LsapArgs a, int32_t n) {
+    __shared__ float s_tile[kTile][kTile + 1];
+    __shared__ MRed s_red[kLsapWaves];
+    __shared__ MRed s_win;
+    __shared__ int s_bad;
+    __shared__ int s_nsc;
+    __shared__ int32_t s_sc[4096];           // this workgroup's visited columns (SC)
+
+    const int G = a.multi_g;
+    // keep a problem's G workgroups on one XCD (dispatch order round-robins
+    // workgroups over the 8 XCDs): p's workgroups are b = xcd + 8 * (q*G + g)
+    const int b = blockIdx.x, xcd = b % 8, qg = b / 8;
+    const int p = xcd + 8 * (qg / G), g = qg % G;
+    if (p >= n) return;
+    const int t = threadIdx.x, lane = t % 64, wave = t / 64;
+    const int64_t R = a.dims[2 * p], K = a.dims[2 * p + 1];
+    if (R == 0 || K == 0 || (R > K ? R : K) <= a.wave_max_cols) return;
+    const bool transpose = K < R;
+    const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
+    const int64_t c0 = nc * g / G, c1 = nc * (g + 1) / G;   // owned columns [c0, c1)
+    const Layout L = lsap_layout(nr, nc, transpose);
+    unsigned char *w = a.ws + a.ws_offs[p];
+    const float *C0 = a.cost + a.cost_offs[p];
+    double *spc = reinterpret_cast<double *>(w + L.spc);
+    double *v = reinterpret_cast<double *>(w + L.v);
+    int32_t *path = reinterpret_cast<int32_t *>(w + L.path);
+    int32_t *row4col = reinterpret_cast<int32_t *>(w + L.row4col);
+    int32_t *pos = reinterpret_cast<int32_t *>(w + L.pos);
+    double *u = reinterpret_cast<double *>(w + L.u);
+    int32_t *col4row = reinterpret_cast<int32_t *>(w + L.col4row);
+    const float *Ct = transpose ? reinterpret_cast<const float *>(w + L.ct) : C0;
+    SyncBlock *sb = reinterpret_cast<SyncBlock *>(a.sync + (size_t)p * kSyncBytes);
+    unsigned int gen = 0;
+
+    // ---- validate, transpose the owned columns, init owned state ----------
+    if (t == 0) s_bad = 0;
+    __syncthreads();
+    int bad = 0;
+    if (transpose) {
+        float *Ctw = reinterpret_cast<float *>(w + L.ct);   // [nr][nc] = C0^T
+        for (int64_t r0 = c0; r0 < c1; r0 += kTile) {         // rows of C0 = owned columns
+            for (int64_t cc0 = 0; cc0 < K; cc0 += kTile) {
+                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                    const int rr = x / kTile, cc = x % kTile;
+                    float val = 0.f;
+                    if (r0 + rr < c1 && cc0 + cc < K) {
+                        val = C0[(r0 + rr) * K + cc0 + cc];
+                        bad |= (val != val) || (val == -INFINITY);
+                    }
+                    s_tile[rr][cc] = val;
+                }
+                __syncthreads();
+                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                    const int cc = x / kTile, rr = x % kTile;
+                    if (r0 + rr < c1 && cc0 + cc < K) Ctw[(cc0 + cc) * nc + r0 + rr] = s_tile[rr][cc];
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        for (int64_t i = 0; i < R; ++i)
+            for (int64_t j = c0 + t; j < c1; j += kLsapThreads) {
+                const float val = C0[i * K + j];
+                bad |= (val != val) || (val == -INFINITY);
+            }
+    }
+    if (bad) atomicOr(&s_bad, 1);
+    for (int64_t j = c0 + t; j < c1; j += kLsapThreads) {
+        v[j] = 0.0;
+        row4col[j] = -1;
+        path[j] = -1;
+    }
+    if (g == 0)
+        for (int64_t i = t; i < nr; i += kLsapThreads) {
+            u[i] = 0.0;
+            col4row[i] = -1;
+        }
+    __syncthreads();
+    if (t == 0 && s_bad) atomicOr(&sb->flag, 1);
+    if (!group_barrier(sb, (++gen) * G)) goto timeout;
+    if (__hip_atomic_load(&sb->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1) {
+        if (g == 0 && t == 0) a.status[p] = 1;
+        return;
+    }
+
+    for (int cur = 0; cur < nr; ++cur) {
+        for (int64_t j = c0 + t; j < c1; j += kLsapThreads) {
+            spc[j] = INFINITY;
+            pos[j] = (int32_t)(nc - 1 - j);   // scan array starts in reverse column order
+        }
+        if (t == 0) s_nsc = 0;
+        int i = cur, sink = -1, step = 0;
+        int64_t nrem = nc;
+        double min_val = 0.0;
+        __syncthreads();
+        while (sink < 0) {
+            const double ui = u[i];
+            const float *Ci = Ct + (int64_t)i * nc;
+            MRed best{INFINITY, 0x7FFFFFFF, -1, -1, -1, -1, -1};
+            for (int64_t j = c0 + t; j < c1; j += kLsapThreads) {
+                const int32_t pj = pos[j];
+                if (pj < 0) continue;
+                if (pj == nrem - 1) best.last_col = (int32_t)j;
+                const double r = ((min_val + (double)Ci[j]) - ui) - v[j];
+                double sj = spc[j];
+                if (r < sj) {
+                    path[j] = i;
+                    spc[j] = r;
+                    sj = r;
+                }
+                const int32_t r4 = row4col[j];
+                if (sj < best.m) {
+                    best.m = sj;
+                    best.first = pj;
+                    best.first_col = (int32_t)j;
+                    best.first_r4 = r4;
+                    best.last_free = r4 == -1 ? pj : -1;
+                    best.last_free_col = r4 == -1 ? (int32_t)j : -1;
+                } else if (sj == best.m) {
+                    if (pj < best.first) {
+                        best.first = pj;
+                        best.first_col = (int32_t)j;
+                        best.first_r4 = r4;
+                    }
+                    if (r4 == -1 && pj > best.last_free) {
+                        best.last_free = pj;
+                        best.last_free_col = (int32_t)j;
+                    }
+                }
+            }
+            best = mred_wave(best);
+            if (lane == 0) s_red[wave] = best;
+            __syncthreads();
+            if (t == 0) {
+                MRed r = s_red[0];
+                for (int k = 1; k < kLsapWaves; ++k) r = mred_combine(r, s_red[k]);
+                sb->slot[step & 1][g] = r;
+            }
+            if (!group_barrier(sb, (++gen) * G)) goto timeout;
+            if (t == 0) {
+                MRed r = sb->slot[step & 1][0];
+                for (int k = 1; k < G; ++k) r = mred_combine(r, sb->slot[step & 1][k]);
+                s_win = r;
+            }
+            __syncthreads();
+            const MRed r = s_win;
+            ++step;
+            if (!(r.m < INFINITY)) {
+                if (g == 0 && t == 0) a.status[p] = 2;   // infeasible
+                return;
+            }
+            const bool use_free = r.last_free >= 0;
+            const int32_t index = use_free ? r.last_free : r.first;
+            const int32_t j = use_free ? r.last_free_col : r.first_col;
+            const int32_t r4 = use_free ? -1 : r.first_r4;
+            --nrem;
+            if (t == 0) {
+                // swap-with-last removal, owner-local; when last == j, j ends removed
+                if (r.last_col >= c0 && r.last_col < c1) pos[r.last_col] = index;
+                if (j >= c0 && j < c1) {
+                    pos[j] = -1;
+                    if (s_nsc < 4096) s_sc[s_nsc] = j;
+                    ++s_nsc;
+                }
+            }
+            min_val = r.m;
+            if (r4 == -1) sink = j;
+            else i = r4;
+            __syncthreads();
+        }
+        // dual updates, column-driven: a visited row i != cur is row4col[j] of
+        // exactly one visited column j, and col4row[i] == j
+        const int nsc = s_nsc;
+        if (nsc > 4096) {                      // SC list overflow: cannot happen for nr <= 4096
+            if (t == 0) atomicExch(&sb->flag, 3);
+            goto timeout;
+        }
+        for (int k = t; k < nsc; k += kLsapThreads) {
+            const int32_t j = s_sc[k];
+            const int32_t ri = row4col[j];
+            if (ri != -1) u[ri] += min_val - spc[j];
+            v[j] -= min_val - spc[j];
+        }
+        if (g == 0 && t == 0) u[cur] += min_val;
+        if (!group_barrier(sb, (++gen) * G)) goto timeout;
+        if (g == 0 && t == 0) {      // augment along the path
+            int j = sink;
+            while (true) {
+                const int i2 = path[j];
+                row4col[j] = i2;
+                const int prev = col4row[i2];
+                col4row[i2] = j;
+                j = prev;
+                if (i2 == cur) break;
+            }
+        }
+        if (!group_barrier(sb, (++gen) * G)) goto timeout;
+    }
+
+    if (g == 0) {   // output pairs in scipy's order
+        const int64_t o = a.out_offs[p];
+        if (transpose) {
+            for (int64_t k = t; k < nr; k += kLsapThreads) {
+                const int32_t rk = col4row[k];
+                int64_t rank = 0;
+                for (int64_t k2 = 0; k2 < nr; ++k2) rank += col4row[k2] < rk;
+                a.row_ind[o + rank] = rk;
+                a.col_ind[o + rank] = k;
+            }
+        } else {
+            for (int64_t i = t; i < nr; i += kLsapThreads) {
+                a.row_ind[o + i] = i;
+                a.col_ind[o + i] = col4row[i];
+            }
+        }
+        if (t == 0) a.status[p] = 0;
+    }
+    return;
+timeout:
+    if (g == 0 && t == 0) a.status[p] = 3;
+}
+
 }  // namespace
 
 extern "C" {
@@ -525,7 +847,8 @@ int64_t mvm_lsap_plan(int32_t n_problems, const int64_t *rows, const int64_t *co
     }
     ws_offs[n_problems] = w;
     out_offs[n_problems] = o;
-    return w;
+    // barrier + reduction slots of lsap_multi_kernel, at the END of the workspace
+    return w + (int64_t)n_problems * (int64_t)kSyncBytes;
 }
 
 int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const int64_t *dims_dev,
@@ -544,9 +867,14 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
     // (0 disables it; capped at 1024)
     int wave_max = mvm_env_int("MVM_LSAP_WAVE_MAX_COLS", kWaveMaxCols);
     wave_max = wave_max < 0 ? 0 : (wave_max > kWaveMaxCols ? kWaveMaxCols : wave_max);
+    const size_t sync_bytes = (size_t)n_problems * kSyncBytes;
+    if (workspace_bytes < sync_bytes) return mvm_fail(MVM_ERR_WORKSPACE, "workspace smaller than the plan");
     LsapArgs a{cost_dev, cost_offs_dev, dims_dev, ws_offs_dev,
                reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
-               col_ind_dev, status_dev, wave_max};
+               col_ind_dev, status_dev, wave_max, 0,
+               reinterpret_cast<unsigned char *>(
+                   (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
+                   ~(uintptr_t)255)};   // at or after the per-problem regions (all 256-aligned)
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (wave_max > 0) {
         const dim3 grid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
@@ -556,6 +884,38 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
         if (wave_max > 128) lsap_wave_kernel<4><<<grid, block, 0, s>>>(a, n_problems);
         if (wave_max > 256) lsap_wave_kernel<8><<<grid, block, 0, s>>>(a, n_problems);
         if (wave_max > 512) lsap_wave_kernel<16><<<grid, block, 0, s>>>(a, n_problems);
+    }
+    // Few large problems: G co-resident workgroups per problem (cooperative
+    // launch guarantees co-residency).  MVM_LSAP_MULTI_G: -1 auto (default),
+    // 0/1 off, 2..16 forced.  Auto uses as many workgroups per problem as the
+    // chip holds, up to 16, when that is at least 2.
+    int G = mvm_env_int("MVM_LSAP_MULTI_G", -1);
+    const int64_t groups8 = ((int64_t)n_problems + 7) / 8;     // problems per XCD slot
+    int occ = 0, cus = 0, dev = 0;
+    if (G != 0 && G != 1 && hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, reinterpret_cast<const void *>(&lsap_multi_kernel),
+                                                     kLsapThreads, 0) == hipSuccess) {
+        const int64_t capacity = (int64_t)cus * occ;
+        const int64_t fit = capacity / (8 * groups8);
+        if (G < 0) G = (int)(fit > kMultiMaxG ? kMultiMaxG : fit);
+        if (G > kMultiMaxG) G = kMultiMaxG;
+        if ((int64_t)G > fit) G = (int)fit;   // never exceed co-residency
+    } else {
+        G = 0;
+    }
+    if (G >= 2) {
+        a.multi_g = G;
+        if (hipMemsetAsync(a.sync, 0, sync_bytes, s) != hipSuccess)
+            return mvm_fail(MVM_ERR_HIP, "hipMemsetAsync(lsap sync) failed");
+        int32_t n_arg = n_problems;
+        void *params[] = {&a, &n_arg};
+        const dim3 grid((unsigned)(8 * G * groups8)), block(kLsapThreads);
+        if (hipLaunchCooperativeKernel(reinterpret_cast<const void *>(&lsap_multi_kernel), grid, block,
+                                       params, 0, s) != hipSuccess) {
+            (void)hipGetLastError();
+            a.multi_g = 0;                     // fall back to one workgroup per problem
+        }
     }
     lsap_kernel<<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");

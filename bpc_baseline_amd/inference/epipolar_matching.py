@@ -134,7 +134,8 @@ def compute_cost_matrix(dets1, dets2, dets3, F12, F13, F23, img1=None, img2=None
     return cubes[0]
 
 
-_LSAP_ERRORS = {1: "matrix contains invalid numeric entries", 2: "cost matrix is infeasible"}
+_LSAP_ERRORS = {1: "matrix contains invalid numeric entries", 2: "cost matrix is infeasible",
+                3: "assignment workgroups failed to synchronise (internal error)"}
 
 
 def linear_sum_assignment(cost_matrix):

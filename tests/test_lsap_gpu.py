@@ -22,11 +22,18 @@ def _batched(cuda, mats):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-@pytest.fixture(params=["wave", "workgroup"])
+@pytest.fixture(params=["default", "workgroup", "multi"])
 def lsap_path(request, monkeypatch):
-    """Problems with a long side <= 1024 run one per wave by default; the
-    workgroup kernel solves the rest (and everything when the knob is 0)."""
-    monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "1024" if request.param == "wave" else "0")
+    """default: long sides <= 1024 one problem per wave, larger ones split over
+    co-resident workgroups when the batch leaves room; workgroup: one
+    1024-thread workgroup per problem; multi: every problem split over 4
+    workgroups."""
+    if request.param == "workgroup":
+        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
+        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+    elif request.param == "multi":
+        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
+        monkeypatch.setenv("MVM_LSAP_MULTI_G", "4")
     return request.param
 
 
@@ -72,11 +79,13 @@ def test_error_statuses(cuda, lsap_path):
     assert list(c) == [1, 0]
 
 
-def test_full_256_cube_equals_scipy(cuda):
+@pytest.mark.parametrize("multi_g", ["-1", "0", "16"])
+def test_full_256_cube_equals_scipy(cuda, monkeypatch, multi_g):
     """Config-2 scale: the (65536 x 256) flattened 256^3 cube of one scene."""
     from bpc_baseline_amd.synth import make_scenes
     from bpc_baseline_amd.inference.epipolar_matching import linear_sum_assignment
     from oracle import oracle as O
+    monkeypatch.setenv("MVM_LSAP_MULTI_G", multi_g)
     b = make_scenes(1, 3, 256, seed=42)
     cube, _, _, _, _ = O.cube(b.pts, b.cam_offs, b.F, 1)
     flat = cube.reshape(256 * 256, 256)

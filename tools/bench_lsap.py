@@ -32,6 +32,9 @@ def gpu_run(k):
     assert int(st.max()) == 0
     return e0.elapsed_time(e1) * 1e-3, r.cpu().numpy(), c.cpu().numpy()
 
+os.environ["MVM_LSAP_MULTI_G"] = "0"
+t1w, _, _ = gpu_run(1)
+os.environ.pop("MVM_LSAP_MULTI_G")
 t1, r1, c1 = gpu_run(1)
 host0 = cube[: n * n * n].cpu().numpy().reshape(n * n, n)
 ts = time.perf_counter(); r0, c0 = scipy_lsa(host0); ts = time.perf_counter() - ts
@@ -41,6 +44,6 @@ tb, rb, cb = gpu_run(b.n_scenes)
 last = cube[tp.cube_offs_host[-2]:tp.cube_offs_host[-1]].cpu().numpy().reshape(n * n, n)
 rl, cl = scipy_lsa(last)
 assert np.array_equal(rb[-n:], rl) and np.array_equal(cb[-n:], cl)
-print(f"{n}^3 single scene: GPU {t1 * 1e3:.2f} ms, scipy {ts * 1e3:.1f} ms on this host "
+print(f"{n}^3 single scene: GPU {t1 * 1e3:.2f} ms (one workgroup: {t1w * 1e3:.2f} ms), scipy {ts * 1e3:.1f} ms on this host "
       f"({ts / t1:.0f}x); batch of {b.n_scenes}: {tb * 1e3:.1f} ms = {b.n_scenes / tb:.0f} scenes/s "
       f"(scipy {1 / ts:.1f} scenes/s on one core)")
