@@ -73,7 +73,9 @@ class MatchBatch:
 def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                    img_offs: torch.Tensor, Ks: np.ndarray, RTs: np.ndarray, *,
                    conf_thresh: float = 0.1, matching_threshold: float = 30,
-                   keep_cube: bool = False, timings: Optional[dict] = None) -> MatchBatch:
+                   keep_cube: bool = False, timings: Optional[dict] = None,
+                   F: Optional[torch.Tensor] = None,
+                   proj: Optional[torch.Tensor] = None) -> MatchBatch:
     """Detect-packing + matching + triangulation of S 3-camera captures.
 
     ``boxes`` f32 [n, 4] xyxy, ``conf``/``cls`` f32 [n]: the detector outputs
@@ -81,6 +83,11 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     device; ``img_offs`` int64 [3S + 1] device.  ``Ks`` float32 [S, 3, 3, 3],
     ``RTs`` float64 [S, 3, 4, 4] (host).  Defaults are PoseEstimatorParams'
     (process_pose.py:36-37).
+
+    ``F`` (f64 [S*3, 9], F12/F13/F23 per capture) and ``proj`` (f64 [S, 3, 3, 4])
+    may be passed as device tensors when the rigs repeat across batches (a
+    static camera rig): they are then not recomputed on the host.  They must
+    be what ``fundamental_matrices_batched`` / ``projection_matrices`` return.
     """
     dev = boxes.device
     import time
@@ -104,9 +111,10 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                                                                    conf_thresh)
     mark("pack")
     # host work while the packing runs: F and P for every capture
-    F = fundamental_matrices_batched(Ks, RTs, camera_pairs(3))
-    F_dev = torch.from_numpy(F.reshape(-1)).to(dev, non_blocking=False)
-    proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev)
+    if F is None:
+        F = torch.from_numpy(fundamental_matrices_batched(Ks, RTs, camera_pairs(3))).to(dev)
+    F_dev = F.reshape(-1)
+    proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev) if proj is None else proj
     mark("F+P host")
 
     counts_host = counts.cpu().numpy().astype(np.int64)

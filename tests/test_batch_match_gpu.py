@@ -103,6 +103,18 @@ def test_batch_vs_oracle_synthetic(cuda):
             np.testing.assert_allclose(gt, rt, rtol=DLT_RTOL, atol=DLT_ATOL)
         total += len(ref)
     assert total > 2 * S     # the synthetic objects are actually recovered
+    # a static rig: F and P passed in give the same results
+    from bpc_baseline_amd.inference.batch_match import match_captures, projection_matrices
+    from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs, fundamental_matrices_batched
+    Fd = torch.from_numpy(fundamental_matrices_batched(Ks, RTs, camera_pairs(3))).to(cuda)
+    Pd = torch.from_numpy(projection_matrices(Ks, RTs)).to(cuda)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    res2 = match_captures(t(boxes), t(conf), t(cls), t(offs), Ks, RTs, F=Fd, proj=Pd)
+    assert np.array_equal(res2.count, res.count)
+    for s in range(S):       # rows past count[s] are unused capacity
+        o, k = int(res.offs[s]), int(res.count[s])
+        assert torch.equal(res2.match[o:o + k], res.match[o:o + k])
+        assert torch.equal(res2.X[o:o + k], res.X[o:o + k])
 
 
 def test_batch_threshold_inf_and_empty(cuda, golden):
