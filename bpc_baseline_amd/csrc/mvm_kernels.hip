@@ -934,6 +934,224 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
     }
 }
 
+// ------------------------------------------- fused tiled cube (v4) ----
+// triplet_tile_kernel without the fp64 workspace: the prologue computes the
+// tile's pair residuals from the centroids and F directly (exactly row_safe's
+// arithmetic) instead of loading them -- e23 for the wave's RPW j rows and the
+// lane's 4 k into registers, e13 [IB][P] and e12 [IB][4*RPW] into LDS -- so
+// the cube costs one launch and no workspace write + read (the
+// workspace was ~10% of the cube's HBM traffic at 256^3).
+struct CubeFusedArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;            // [S*3, 9]: F12, F13, F23
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t j_blocks, i_blocks;
+};
+
+struct LineRec {
+    double l0, l1, l2;
+    double deg;                 // 1.0: degenerate line (9999 sentinel)
+};
+
+__device__ __forceinline__ double pair_e(const LineRec &col, const LineRec &row, double rx,
+                                         double ry, double cx, double cy) {
+    const double d1 = col.deg != 0.0 ? kSentinel : line_dist(col.l0, col.l1, col.l2, rx, ry);
+    const double d2 = row.deg != 0.0 ? kSentinel : line_dist(row.l0, row.l1, row.l2, cx, cy);
+    return 0.5 * (d1 + d2);                                                       // :28
+}
+
+__device__ __forceinline__ void load_f(const double *F, double f[9]) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) f[q] = F[q];
+}
+
+template <int kCubeIB, int kCubeRPW>
+__global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs args) {
+    constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
+    __shared__ LineRec s_r13[kCubeIB], s_r12[kCubeIB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[kCubeIB][2], s_p1[kJ][2];
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blockIdx.x / per_scene);
+    const int rem = (int)(blockIdx.x % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
+    const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
+    const int jw0 = jb * kJ;
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;
+    const int nrows = min(kCubeRPW, M - j0);
+    const int kb = kColsPerLane * lane;
+    const int kvalid = P - kb;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    const bool full = (P == kChunk) && ((coff & 3) == 0) && args.cube;
+    const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
+    const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
+    const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
+
+    // ---- prologue 1: the tile's view-0 rows and view-1 rows/columns --------
+    if (t < kCubeIB) {
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (t < ni) {
+            double f[9];
+            px = args.pts[2 * (c0 + i0 + t)];
+            py = args.pts[2 * (c0 + i0 + t) + 1];
+            load_f(F13, f);
+            a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F12, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_r13[t] = a;
+        s_r12[t] = b;
+        s_p0[t][0] = px;
+        s_p0[t][1] = py;
+    } else if (t >= kWave && t < kWave + kJ) {
+        const int jj = t - kWave;
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (jw0 + jj < M) {
+            double f[9];
+            px = args.pts[2 * (c1 + jw0 + jj)];
+            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            load_f(F12, f);
+            a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_c12[jj] = a;
+        s_r23[jj] = b;
+        s_p1[jj][0] = px;
+        s_p1[jj][1] = py;
+    }
+    __syncthreads();
+    // ---- prologue 2: the tile's pair residuals (row_safe's arithmetic) -------
+    {
+        const int k = t;                                   // kThreads == kChunk: one column each
+        if (k < P) {
+            double f[9];
+            load_f(F13, f);
+            const double x = args.pts[2 * (c2 + k)], y = args.pts[2 * (c2 + k) + 1];
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+#pragma unroll 4
+            for (int r = 0; r < kCubeIB; ++r)
+                s13[r][k] = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+        } else {
+            for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
+        }
+    }
+    for (int x = t; x < kCubeIB * kJ; x += kThreads) {
+        const int r = x / kJ, jj = x % kJ;
+        s12[r][jj] = (r < ni && jw0 + jj < M)
+                         ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                         : 0.0;
+    }
+    double a23[kCubeRPW][kColsPerLane];
+    {
+        double f[9];
+        load_f(F23, f);
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) {
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            double x = 0.0, y = 0.0;
+            if (q < kvalid) {
+                x = args.pts[2 * (c2 + kb + q)];
+                y = args.pts[2 * (c2 + kb + q) + 1];
+                cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                const int jj = wave * kCubeRPW + r;
+                a23[r][q] = (r < nrows && q < kvalid)
+                                ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
+                                : 0.0;
+            }
+        }
+    }
+    __syncthreads();
+    if (nrows <= 0) return;   // after the barrier: no more barriers below
+
+    for (int ii = 0; ii < ni; ++ii) {
+        const int i = i0 + ii;
+        double a13[kColsPerLane];
+        {
+            const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+            const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+            a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+        }
+        uint32_t key[kCubeRPW];
+        int32_t idx[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            key[r] = kKeyInvalid;
+            idx[r] = 0x7FFFFFFF;
+            if (r >= nrows) continue;   // uniform
+            const double v12 = s12[ii][wave * kCubeRPW + r];
+            double sum[kColsPerLane], q0[kColsPerLane];
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                q0[q] = sum[q] * kThird;
+                ok &= third_fast_ok(q0[q]);
+            }
+            float v[kColsPerLane];
+            const int64_t row = (int64_t)i * M + j0 + r;
+            if (full && __all(ok)) {
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                              (uint32_t)kb * 4u, v);
+                Best b{v[0], kb};
+#pragma unroll
+                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                key[r] = __float_as_uint(b.v) + 1u;
+                idx[r] = b.j;
+            } else {
+                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    v[q] = (float)qq;
+                    if (q < kvalid) {
+                        if (args.cube)
+                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                        best_update_safe(b, v[q], kb + q);
+                    }
+                }
+                key[r] = best_key(b);
+                idx[r] = b.j;
+            }
+        }
+        uint32_t kmin[kCubeRPW];
+        int32_t imin[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            kmin[r] = kKeyInvalid;
+            imin[r] = 0;
+            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+        }
+        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                    roff + (int64_t)i * M + j0);
+    }
+}
+
 // ------------------------------------------------- small-scene cube ----
 // Scenes whose views hold at most kSmallMaxN detections (the IPD regime: a
 // few to a few dozen objects per image) are too small for the tiled kernel's
@@ -1192,6 +1410,7 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
 //   MVM_PAIRWISE_NT   row store policy: 1 nt (default), 0 default, 2 sc1, 3 sc0 sc1
 //   MVM_TRIPLET_SMALL 1: one-workgroup-per-scene cube for views of <= 64
+//   MVM_TRIPLET_FUSED 1: tiled cube with in-prologue pair residuals (<= 256)
 //   MVM_LSAP_WAVE_MAX_COLS  long-side limit of the one-wave LSAP (mvm_lsap.hip)
 int env_int(const char *name, int dflt) {
     const char *e = getenv(name);
@@ -1461,6 +1680,36 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                         (long long)blocks);
         triplet_small_kernel<<<dim3((unsigned)blocks), dim3(kThreads), lds, s>>>(c);
         return check_launch("triplet_small_kernel");
+    }
+    if (max_n <= kChunk && variant == 3 && env_int("MVM_TRIPLET_FUSED", 1)) {
+        // tiles of 16 i x 32 j whose pair residuals are computed in the prologue
+        CubeFusedArgs c{};
+        c.pts = pts_dev;
+        c.cam_offs = cam_offs_dev;
+        c.F = F_dev;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        // MVM_TRIPLET_TILE: 3 = 16 i x 32 j (default), 4 = 32 i x 32 j, 2 = 8 i x 32 j, 0 = 16 i x 16 j
+        const int tile = env_int("MVM_TRIPLET_TILE", 3);
+        const int ib = tile == 4 ? 32 : (tile == 2 ? 8 : 16);
+        const int rpw = tile == 0 ? 4 : 8;
+        c.j_blocks = (max_n + kWaves * rpw - 1) / (kWaves * rpw);
+        c.i_blocks = (max_n + ib - 1) / ib;
+        const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
+        if (blocks > 0x7FFFFFFFLL)
+            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+        const dim3 grid((unsigned)blocks), block(kThreads);
+        switch (tile) {
+        case 4: triplet_fused_kernel<32, 8><<<grid, block, 0, s>>>(c); break;
+        case 2: triplet_fused_kernel<8, 8><<<grid, block, 0, s>>>(c); break;
+        case 0: triplet_fused_kernel<16, 4><<<grid, block, 0, s>>>(c); break;
+        default: triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c); break;
+        }
+        return check_launch("triplet_fused_kernel");
     }
     const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;
     const int64_t mat_stride = (int64_t)max_n * ld;

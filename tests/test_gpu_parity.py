@@ -136,11 +136,13 @@ def test_pairwise_argmin_only(cuda):
 
 
 # --------------------------------------------------------------- cube ----
-@pytest.fixture(params=["small", "tiled"])
+@pytest.fixture(params=["small", "fused", "tiled"])
 def cube_path(request, monkeypatch):
-    """Run a cube test through the one-workgroup-per-scene kernel (views of
-    <= 64 detections) and through the tiled kernel + fp64 workspace."""
+    """Run a cube test through each cube kernel: the small-scene kernel (views
+    of <= 64 detections), the fused tiled kernel (pair residuals computed in
+    the prologue; default up to 256) and the tiled kernel + fp64 workspace."""
     monkeypatch.setenv("MVM_TRIPLET_SMALL", "1" if request.param == "small" else "0")
+    monkeypatch.setenv("MVM_TRIPLET_FUSED", "0" if request.param == "tiled" else "1")
     return request.param
 
 
