@@ -379,7 +379,7 @@ def main():
         "roofline": {
             "bound": "hbm",
             "kernel": ("pairwise_kernel" if wl["mode"] == "pairwise"
-                       else "triplet_tile_kernel + pairwise_kernel<f64> prologue (one op)"),
+                       else "triplet_fused_kernel"),
             "achieved": achieved_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
