@@ -1355,6 +1355,25 @@ __global__ __launch_bounds__(kThreads) void write_probe_pol_kernel(f32x4 *dst, s
     }
 }
 
+// the pairwise kernel's store ORDER on a 256 KiB block per workgroup: 64 rows
+// of 4 KiB, wave w owns rows 16w..16w+15 and walks chunk-outer / row-inner
+// (consecutive stores of a wave are 4 KiB apart); ROWMAJOR = 1 walks each
+// row's 4 chunks first (consecutive stores contiguous)
+template <bool ROWMAJOR>
+__global__ __launch_bounds__(kThreads) void write_probe_rows_kernel(f32x4 *dst, size_t n16, float val) {
+    const f32x4 v = {val, val, val, val};
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const size_t base = (size_t)blockIdx.x * (64 * 256);         // 16-byte units: 64 rows x 256
+    for (int a = 0; a < 16; ++a) {
+        for (int b = 0; b < 4; ++b) {
+            const int row = wave * 16 + (ROWMAJOR ? a : (a % 4) * 4 + b) ;
+            const int chunk = ROWMAJOR ? b : a / 4;
+            const size_t i = base + (size_t)row * 256 + chunk * 64 + lane;
+            if (i < n16) __builtin_nontemporal_store(v, dst + i);
+        }
+    }
+}
+
 // grid-stride variant: a fixed grid of `waves per CU` x 256 CUs workgroups
 template <bool NT>
 __global__ __launch_bounds__(kThreads) void write_probe_stride_kernel(f32x4 *dst, size_t n16,
@@ -1604,7 +1623,8 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
     const size_t n16 = bytes / 16;
     // MVM_PROBE_MODE (experiments): 0 nt 16 KiB/WG (the residual kernels' form),
     // 1 plain 16 KiB/WG, 2 nt 64 KiB/WG, 3 plain 64 KiB/WG, 4 nt grid-stride, 5 plain grid-stride,
-    // 6 sc1, 7 sc0 sc1, 8 nt sc1 (16 KiB/WG)
+    // 6 sc1, 7 sc0 sc1, 8 nt sc1 (16 KiB/WG), 9 / 10 the pairwise kernel's row order
+    // (chunk-outer / row-major) on 256 KiB per WG
     const int mode = env_int("MVM_PROBE_MODE", 0);
     const int per = (mode == 2 || mode == 3) ? 16 : 4;
     const size_t blocks = (n16 + per * kThreads - 1) / (per * kThreads);
@@ -1622,6 +1642,8 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         case 6: write_probe_pol_kernel<1><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 7: write_probe_pol_kernel<2><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 8: write_probe_pol_kernel<3><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 9: write_probe_rows_kernel<false><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 10: write_probe_rows_kernel<true><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
         default: write_probe_kernel<4, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
     }
     return check_launch("write_probe_kernel");
