@@ -51,6 +51,7 @@ struct LsapArgs {
     int32_t *status;            // 0 ok, 1 invalid entries (NaN / -inf), 2 infeasible
     int32_t wave_max_cols;      // problems with max(rows, cols) <= this run in lsap_wave_kernel
     int32_t multi_g;            // > 1: larger problems run in lsap_multi_kernel, G workgroups each
+    int32_t mid_max_cols;       // long sides in (wave_max_cols, this]: 256-thread lsap_kernel
     unsigned char *sync;        // per-problem barrier + reduction slots (multi kernel)
 };
 
@@ -109,9 +110,11 @@ __host__ __device__ inline Layout lsap_layout(int64_t nr, int64_t nc, bool trans
     return L;
 }
 
-__global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
+template <int NT>
+__global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
+    constexpr int kNW = NT / 64;
     __shared__ float s_tile[kTile][kTile + 1];
-    __shared__ Red s_red[kLsapWaves];
+    __shared__ Red s_red[kNW];
     __shared__ int s_flag;
     __shared__ int s_i, s_sink, s_nrem, s_nsr, s_nsc;
     __shared__ double s_min;
@@ -126,6 +129,8 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
     }
     if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
     if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
+    const int64_t longside = R > K ? R : K;
+    if ((longside <= a.mid_max_cols) != (NT < kLsapThreads)) return;   // the other class
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const Layout L = lsap_layout(nr, nc, transpose);
@@ -151,7 +156,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
         float *Ctw = reinterpret_cast<float *>(w + L.ct);   // [nr][nc] = C0^T
         for (int64_t r0 = 0; r0 < R; r0 += kTile) {
             for (int64_t c0 = 0; c0 < K; c0 += kTile) {
-                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                for (int x = t; x < kTile * kTile; x += NT) {
                     const int rr = x / kTile, cc = x % kTile;
                     float val = 0.f;
                     if (r0 + rr < R && c0 + cc < K) {
@@ -161,7 +166,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
                     s_tile[rr][cc] = val;
                 }
                 __syncthreads();
-                for (int x = t; x < kTile * kTile; x += kLsapThreads) {
+                for (int x = t; x < kTile * kTile; x += NT) {
                     const int cc = x / kTile, rr = x % kTile;
                     if (r0 + rr < R && c0 + cc < K) Ctw[(c0 + cc) * nc + r0 + rr] = s_tile[rr][cc];
                 }
@@ -169,18 +174,18 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
             }
         }
     } else {
-        for (int64_t x = t; x < R * K; x += kLsapThreads) {
+        for (int64_t x = t; x < R * K; x += NT) {
             const float val = C0[x];
             bad |= (val != val) || (val == -INFINITY);
         }
     }
     if (bad) atomicOr(&s_flag, 1);
-    for (int64_t j = t; j < nc; j += kLsapThreads) {
+    for (int64_t j = t; j < nc; j += NT) {
         v[j] = 0.0;
         row4col[j] = -1;
         path[j] = -1;
     }
-    for (int64_t i = t; i < nr; i += kLsapThreads) {
+    for (int64_t i = t; i < nr; i += NT) {
         u[i] = 0.0;
         col4row[i] = -1;
     }
@@ -192,7 +197,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
 
     // ---- one shortest augmenting path per short-side row --------------------
     for (int cur = 0; cur < nr; ++cur) {
-        for (int64_t j = t; j < nc; j += kLsapThreads) {
+        for (int64_t j = t; j < nc; j += NT) {
             spc[j] = INFINITY;
             pos[j] = (int32_t)(nc - 1 - j);   // scan array starts in reverse column order
             rem[nc - 1 - j] = (int32_t)j;
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
             const double ui = u[i];
             const float *Ci = Ct + (int64_t)i * nc;
             Red best{INFINITY, 0x7FFFFFFF, -1};
-            for (int64_t j = t; j < nc; j += kLsapThreads) {
+            for (int64_t j = t; j < nc; j += NT) {
                 const int32_t pj = pos[j];
                 if (pj < 0) continue;   // already visited (removed from the scan)
                 const double r = ((min_val + (double)Ci[j]) - ui) - v[j];
@@ -237,7 +242,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
             __syncthreads();
             if (t == 0) {
                 Red r = s_red[0];
-                for (int k = 1; k < kLsapWaves; ++k) r = red_combine(r, s_red[k]);
+                for (int k = 1; k < kNW; ++k) r = red_combine(r, s_red[k]);
                 sr[s_nsr++] = i;
                 if (r.m == INFINITY) {
                     s_flag = 2;   // infeasible (scipy: "cost matrix is infeasible")
@@ -266,11 +271,11 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
         }
         // dual updates (each entry independent: order-free)
         const double min_val = s_min;
-        for (int k = t; k < s_nsr; k += kLsapThreads) {
+        for (int k = t; k < s_nsr; k += NT) {
             const int i = sr[k];
             if (i != cur) u[i] += min_val - spc[col4row[i]];
         }
-        for (int k = t; k < s_nsc; k += kLsapThreads) {
+        for (int k = t; k < s_nsc; k += NT) {
             const int j = sc[k];
             v[j] -= min_val - spc[j];
         }
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
     const int64_t o = a.out_offs[p];
     if (transpose) {
         // (col4row[k], k) sorted by col4row[k] (distinct): rank by counting
-        for (int64_t k = t; k < nr; k += kLsapThreads) {
+        for (int64_t k = t; k < nr; k += NT) {
             const int32_t rk = col4row[k];
             int64_t rank = 0;
             for (int64_t k2 = 0; k2 < nr; ++k2) rank += col4row[k2] < rk;
@@ -302,7 +307,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_kernel(LsapArgs a) {
             a.col_ind[o + rank] = k;
         }
     } else {
-        for (int64_t i = t; i < nr; i += kLsapThreads) {
+        for (int64_t i = t; i < nr; i += NT) {
             a.row_ind[o + i] = i;
             a.col_ind[o + i] = col4row[i];
         }
@@ -871,7 +876,7 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
     if (workspace_bytes < sync_bytes) return mvm_fail(MVM_ERR_WORKSPACE, "workspace smaller than the plan");
     LsapArgs a{cost_dev, cost_offs_dev, dims_dev, ws_offs_dev,
                reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
-               col_ind_dev, status_dev, wave_max, 0,
+               col_ind_dev, status_dev, wave_max, 0, 0,
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
                    ~(uintptr_t)255)};   // at or after the per-problem regions (all 256-aligned)
@@ -917,7 +922,13 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
             a.multi_g = 0;                     // fall back to one workgroup per problem
         }
     }
-    lsap_kernel<<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
+    // one workgroup per problem: 256 threads up to MVM_LSAP_MID_MAX_COLS long-side
+    // columns, 1024 threads above.  Default 0 (always 1024): on MI355X the
+    // 256-thread form tied the wave kernel at 576 x 24 and lost at 4096 x 64
+    // (5.65 vs 5.05 ms per 1000) and 65536 x 256 (200 vs 82 ms per 200)
+    a.mid_max_cols = mvm_env_int("MVM_LSAP_MID_MAX_COLS", 0);
+    lsap_kernel<256><<<dim3((unsigned)n_problems), dim3(256), 0, s>>>(a);
+    lsap_kernel<kLsapThreads><<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");
 }
 
