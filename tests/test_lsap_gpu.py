@@ -22,7 +22,7 @@ def _batched(cuda, mats):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-@pytest.fixture(params=["default", "workgroup", "multi"])
+@pytest.fixture(params=["default", "workgroup", "workgroup256", "multi"])
 def lsap_path(request, monkeypatch):
     """default: long sides <= 1024 one problem per wave, larger ones split over
     co-resident workgroups when the batch leaves room; workgroup: one
@@ -31,6 +31,10 @@ def lsap_path(request, monkeypatch):
     if request.param == "workgroup":
         monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
         monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+    elif request.param == "workgroup256":
+        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
+        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+        monkeypatch.setenv("MVM_LSAP_MID_MAX_COLS", "1000000")
     elif request.param == "multi":
         monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
         monkeypatch.setenv("MVM_LSAP_MULTI_G", "4")
