@@ -48,7 +48,8 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
 
 # ----------------------------------------------------------- pairwise ----
 @pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),
-                                          (4, 3, 37, True), (2, 2, 1, False), (3, 6, 130, True)])
+                                          (4, 3, 37, True), (2, 2, 1, False), (3, 6, 130, True),
+                                          (1, 3, 2500, False), (3, 2, 1500, True), (1, 8, 300, True)])
 def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, C, n, seed=100 + S * n, ragged=ragged)
