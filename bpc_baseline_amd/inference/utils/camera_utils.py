@@ -121,7 +121,12 @@ def fundamental_matrices_batched(Ks: np.ndarray, RTs: np.ndarray, pairs: np.ndar
     skew[..., 1, 0], skew[..., 1, 2] = t_rel[..., 2], -t_rel[..., 0]
     skew[..., 2, 0], skew[..., 2, 1] = -t_rel[..., 1], t_rel[..., 0]
     essential = skew @ R_rel
-    Kinv = np.linalg.inv(Ks)             # once per camera; each matrix solved on its own
+    # inverse once per DISTINCT intrinsic matrix (byte-wise: identical bytes give
+    # identical inverses), as rigs share K across captures
+    flatK = np.ascontiguousarray(Ks, dtype=np.float32).reshape(-1, 9)
+    keys = flatK.view(np.dtype((np.void, flatK.dtype.itemsize * 9))).reshape(-1)
+    _, first, inverse = np.unique(keys, return_index=True, return_inverse=True)
+    Kinv = np.linalg.inv(flatK[first].reshape(-1, 3, 3))[inverse.reshape(-1)].reshape(Ks.shape)
     K1inv, K2inv = Kinv[:, a], Kinv[:, b]
     F = np.swapaxes(K2inv, -1, -2) @ essential @ K1inv
     f22 = F[..., 2:3, 2:3]
