@@ -14,12 +14,13 @@ from __future__ import annotations
 
 import json
 import os
-from typing import Dict, Iterable, Sequence
+from typing import Dict, Iterable, Optional, Sequence
 
 import numpy as np
 
 __all__ = [
     "load_camera_params",
+    "capture_cameras",
     "compute_fundamental_matrix",
     "calc_pose_matrix",
     "camera_pairs",
@@ -27,12 +28,15 @@ __all__ = [
 ]
 
 
-def load_camera_params(scene_dir: str, cam_ids: Iterable[str]) -> Dict[str, Dict[str, dict]]:
+def load_camera_params(scene_dir: str, cam_ids: Iterable[str], verbose: bool = True
+                       ) -> Dict[str, Dict[str, dict]]:
     """Read BOP ``scene_camera_<cam>.json`` files (camera_utils.py:6-20).
 
-    Returns ``{cam: {'K': {im_id: f32[3,3]}, 'R': {im_id: f32[3,3]}, 't': {im_id: f32[3]}}}``.
+    Returns ``{cam: {'K': {im_id: f32[3,3]}, 'R': {im_id: f32[3,3]}, 't': {im_id: f32[3]}}}``
+    and, like the reference, prints the last file read.
     """
     params: Dict[str, Dict[str, dict]] = {}
+    cam = None
     for cam in cam_ids:
         path = os.path.join(scene_dir, f"scene_camera_{cam}.json")
         with open(path) as fh:
@@ -44,7 +48,33 @@ def load_camera_params(scene_dir: str, cam_ids: Iterable[str]) -> Dict[str, Dict
             per_cam["R"][im_id] = np.asarray(rec["cam_R_w2c"], dtype=np.float32).reshape(3, 3)
             per_cam["t"][im_id] = np.asarray(rec["cam_t_w2c"], dtype=np.float32).reshape(-1)
         params[cam] = per_cam
+    if verbose:
+        print(f"Loading camera parameters from: {os.path.join(scene_dir, f'scene_camera_{cam}.json')}")
     return params
+
+
+def capture_cameras(scene_dir: str, cam_ids: Sequence[str], image_ids: Sequence[int], *,
+                    params: Optional[Dict[str, Dict[str, dict]]] = None, verbose: bool = False):
+    """Cameras of many captures of one scene, stacked for ``match_captures``.
+
+    What ``Capture.from_dir`` (bpc/utils/data_utils.py:399-405) builds per
+    capture -- ``Ks = [K[cam][image_id]]`` (float32) and ``RTs =
+    [calc_pose_matrix(R, t)]`` (float64) -- for every ``image_id`` at once,
+    reading each camera's JSON once.  -> (Ks f32 [S, C, 3, 3], RTs f64 [S, C, 4, 4]).
+    """
+    if params is None:
+        params = load_camera_params(scene_dir, cam_ids, verbose=verbose)
+    S, C = len(image_ids), len(cam_ids)
+    Ks = np.empty((S, C, 3, 3), np.float32)
+    RTs = np.zeros((S, C, 4, 4), np.float64)
+    RTs[:, :, 3, 3] = 1.0
+    for c, cam in enumerate(cam_ids):
+        p = params[cam]
+        Ks[:, c] = np.stack([p["K"][i] for i in image_ids]) if S else Ks[:, c]
+        if S:
+            RTs[:, c, :3, :3] = np.stack([p["R"][i] for i in image_ids])
+            RTs[:, c, :3, 3] = np.stack([p["t"][i] for i in image_ids])
+    return Ks, RTs
 
 
 def calc_pose_matrix(R_mat: np.ndarray, t: np.ndarray) -> np.ndarray:

@@ -196,3 +196,26 @@ def test_batched_fundamental_matrices_vs_reference(golden):
     RT[..., :3, :3], RT[..., :3, 3], RT[..., 3, 3] = g["R"], g["t"], 1.0
     got = fundamental_matrices_batched(g["K"], RT, np.array([[0, 1]]))
     np.testing.assert_allclose(got.reshape(-1, 3, 3), g["F"], rtol=1e-12, atol=1e-18)
+
+
+def test_capture_cameras_equals_per_capture(tmp_path, capsys):
+    """Batched camera ingestion == Capture.from_dir's per-capture Ks / RTs."""
+    import json
+    from bpc_baseline_amd.inference.utils.camera_utils import (calc_pose_matrix, capture_cameras,
+                                                                load_camera_params)
+    rng = np.random.default_rng(4)
+    cams = ["cam1", "cam2", "cam3"]
+    for cam in cams:
+        recs = {str(i): {"cam_K": rng.uniform(-2000, 4000, 9).tolist(),
+                         "cam_R_w2c": rng.normal(size=9).tolist(),
+                         "cam_t_w2c": rng.uniform(-2000, 2000, 3).tolist()} for i in range(7)}
+        (tmp_path / f"scene_camera_{cam}.json").write_text(json.dumps(recs))
+    params = load_camera_params(str(tmp_path), cams)
+    assert "Loading camera parameters from:" in capsys.readouterr().out   # as the reference
+    ids = [5, 0, 3]
+    Ks, RTs = capture_cameras(str(tmp_path), cams, ids)
+    for s, im in enumerate(ids):
+        for c, cam in enumerate(cams):
+            assert np.array_equal(Ks[s, c], params[cam]["K"][im]) and Ks.dtype == np.float32
+            ref = calc_pose_matrix(params[cam]["R"][im], params[cam]["t"][im])
+            assert np.array_equal(RTs[s, c], ref) and RTs.dtype == ref.dtype
