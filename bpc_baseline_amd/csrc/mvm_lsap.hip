@@ -38,6 +38,7 @@ namespace {
 constexpr int kLsapThreads = 1024;
 constexpr int kLsapWaves = kLsapThreads / 64;
 constexpr int kTile = 64;   // transpose tile
+constexpr int kScanU = 4;   // columns per thread whose loads are batched in a Dijkstra scan
 
 struct LsapArgs {
     const float *cost;
@@ -113,6 +114,7 @@ __host__ __device__ inline Layout lsap_layout(int64_t nr, int64_t nc, bool trans
 template <int NT>
 __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     constexpr int kNW = NT / 64;
+    constexpr int kU = NT >= 1024 ? kScanU : 2 * kScanU;   // batched loads per thread (VGPR budget)
     __shared__ float s_tile[kTile][kTile + 1];
     __shared__ Red s_red[kNW];
     __shared__ int s_flag;
@@ -217,24 +219,44 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
             const double ui = u[i];
             const float *Ci = Ct + (int64_t)i * nc;
             Red best{INFINITY, 0x7FFFFFFF, -1};
-            for (int64_t j = t; j < nc; j += NT) {
-                const int32_t pj = pos[j];
-                if (pj < 0) continue;   // already visited (removed from the scan)
-                const double r = ((min_val + (double)Ci[j]) - ui) - v[j];
-                double sj = spc[j];
-                if (r < sj) {
-                    path[j] = i;
-                    spc[j] = r;
-                    sj = r;
+            // kU columns per thread per batch: all their loads are issued
+            // before any is used (a load-use chain per column would serialise
+            // the L2 latency)
+            for (int64_t jb = t; jb < nc; jb += (int64_t)NT * kU) {
+                int32_t pj[kU], r4[kU];
+                float cj[kU];
+                double vj[kU], sj[kU];
+#pragma unroll
+                for (int q = 0; q < kU; ++q) {
+                    const int64_t j = jb + (int64_t)q * NT;
+                    const int64_t jc = j < nc ? j : jb;
+                    pj[q] = pos[jc];
+                    cj[q] = Ci[jc];
+                    vj[q] = v[jc];
+                    sj[q] = spc[jc];
+                    r4[q] = row4col[jc];
+                    if (j >= nc) pj[q] = -1;
                 }
-                const bool free_col = row4col[j] == -1;
-                if (sj < best.m) {
-                    best.m = sj;
-                    best.first = pj;
-                    best.last_free = free_col ? pj : -1;
-                } else if (sj == best.m) {
-                    best.first = min(best.first, pj);
-                    if (free_col) best.last_free = max(best.last_free, pj);
+#pragma unroll
+                for (int q = 0; q < kU; ++q) {
+                    if (pj[q] < 0) continue;   // already visited (removed from the scan)
+                    const int64_t j = jb + (int64_t)q * NT;
+                    const double r = ((min_val + (double)cj[q]) - ui) - vj[q];
+                    double sq = sj[q];
+                    if (r < sq) {
+                        path[j] = i;
+                        spc[j] = r;
+                        sq = r;
+                    }
+                    const bool free_col = r4[q] == -1;
+                    if (sq < best.m) {
+                        best.m = sq;
+                        best.first = pj[q];
+                        best.last_free = free_col ? pj[q] : -1;
+                    } else if (sq == best.m) {
+                        best.first = min(best.first, pj[q]);
+                        if (free_col) best.last_free = max(best.last_free, pj[q]);
+                    }
                 }
             }
             best = red_wave(best);
@@ -347,18 +369,28 @@ __device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_
 
     // validate (NaN / -inf, as scipy) and transpose a tall matrix
     int bad = 0;
-    if (transpose) {
+    {
+        // 8 loads per lane in flight, 32-bit index arithmetic (R * Kc <= 2^20)
         float *Ctw = reinterpret_cast<float *>(w + L.ct);   // [nr][nc] = C0^T
-        for (int64_t x = lane; x < R * Kc; x += 64) {
-            const float val = C0[x];
-            bad |= (val != val) || (val == -INFINITY);
-            const int64_t j = x / Kc, i = x - j * Kc;
-            Ctw[i * nc + j] = val;
-        }
-    } else {
-        for (int64_t x = lane; x < R * Kc; x += 64) {
-            const float val = C0[x];
-            bad |= (val != val) || (val == -INFINITY);
+        const uint32_t total = (uint32_t)(R * Kc), kc = (uint32_t)Kc;
+        for (uint32_t x0 = lane; x0 < total; x0 += 64 * 8) {
+            float val[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t x = x0 + 64u * q;
+                val[q] = x < total ? C0[x] : 0.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t x = x0 + 64u * q;
+                if (x < total) {
+                    bad |= (val[q] != val[q]) || (val[q] == -INFINITY);
+                    if (transpose) {
+                        const uint32_t j = x / kc, i = x - j * kc;
+                        Ctw[(int64_t)i * nc + j] = val[q];
+                    }
+                }
+            }
         }
     }
     if (__ballot(bad)) {
@@ -392,11 +424,16 @@ __device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_
         while (sink < 0) {
             const double ui = u[i];
             const float *Ci = Ct + (int64_t)i * nc;
+            // all K cost loads first (a load per slot behind the slot's branch
+            // would serialise K L2 round trips per step)
+            float cq[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) cq[q] = Ci[min(lane + 64 * q, nc - 1)];
             Red best{INFINITY, 0x7FFFFFFF, -1};
 #pragma unroll
             for (int q = 0; q < K; ++q) {
                 if (pos[q] < 0) continue;
-                const double r = ((min_val + (double)Ci[lane + 64 * q]) - ui) - v[q];
+                const double r = ((min_val + (double)cq[q]) - ui) - v[q];
                 if (r < spc[q]) {
                     path[q] = i;
                     spc[q] = r;
@@ -704,34 +741,50 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_multi_kernel(LsapArgs a, in
             const double ui = u[i];
             const float *Ci = Ct + (int64_t)i * nc;
             MRed best{INFINITY, 0x7FFFFFFF, -1, -1, -1, -1, -1};
-            for (int64_t j = c0 + t; j < c1; j += kLsapThreads) {
-                const int32_t pj = pos[j];
-                if (pj < 0) continue;
-                if (pj == nrem - 1) best.last_col = (int32_t)j;
-                const double r = ((min_val + (double)Ci[j]) - ui) - v[j];
-                double sj = spc[j];
-                if (r < sj) {
-                    path[j] = i;
-                    spc[j] = r;
-                    sj = r;
+            for (int64_t jb = c0 + t; jb < c1; jb += (int64_t)kLsapThreads * kScanU) {
+                int32_t pj[kScanU], r4[kScanU];
+                float cj[kScanU];
+                double vj[kScanU], sj[kScanU];
+#pragma unroll
+                for (int q = 0; q < kScanU; ++q) {     // all loads first
+                    const int64_t j = jb + (int64_t)q * kLsapThreads;
+                    const int64_t jc = j < c1 ? j : jb;
+                    pj[q] = pos[jc];
+                    cj[q] = Ci[jc];
+                    vj[q] = v[jc];
+                    sj[q] = spc[jc];
+                    r4[q] = row4col[jc];
+                    if (j >= c1) pj[q] = -1;
                 }
-                const int32_t r4 = row4col[j];
-                if (sj < best.m) {
-                    best.m = sj;
-                    best.first = pj;
-                    best.first_col = (int32_t)j;
-                    best.first_r4 = r4;
-                    best.last_free = r4 == -1 ? pj : -1;
-                    best.last_free_col = r4 == -1 ? (int32_t)j : -1;
-                } else if (sj == best.m) {
-                    if (pj < best.first) {
-                        best.first = pj;
-                        best.first_col = (int32_t)j;
-                        best.first_r4 = r4;
+#pragma unroll
+                for (int q = 0; q < kScanU; ++q) {
+                    if (pj[q] < 0) continue;
+                    const int64_t j = jb + (int64_t)q * kLsapThreads;
+                    if (pj[q] == nrem - 1) best.last_col = (int32_t)j;
+                    const double r = ((min_val + (double)cj[q]) - ui) - vj[q];
+                    double sq = sj[q];
+                    if (r < sq) {
+                        path[j] = i;
+                        spc[j] = r;
+                        sq = r;
                     }
-                    if (r4 == -1 && pj > best.last_free) {
-                        best.last_free = pj;
-                        best.last_free_col = (int32_t)j;
+                    if (sq < best.m) {
+                        best.m = sq;
+                        best.first = pj[q];
+                        best.first_col = (int32_t)j;
+                        best.first_r4 = r4[q];
+                        best.last_free = r4[q] == -1 ? pj[q] : -1;
+                        best.last_free_col = r4[q] == -1 ? (int32_t)j : -1;
+                    } else if (sq == best.m) {
+                        if (pj[q] < best.first) {
+                            best.first = pj[q];
+                            best.first_col = (int32_t)j;
+                            best.first_r4 = r4[q];
+                        }
+                        if (r4[q] == -1 && pj[q] > best.last_free) {
+                            best.last_free = pj[q];
+                            best.last_free_col = (int32_t)j;
+                        }
                     }
                 }
             }
@@ -922,11 +975,11 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
             a.multi_g = 0;                     // fall back to one workgroup per problem
         }
     }
-    // one workgroup per problem: 256 threads up to MVM_LSAP_MID_MAX_COLS long-side
-    // columns, 1024 threads above.  Default 0 (always 1024): on MI355X the
-    // 256-thread form tied the wave kernel at 576 x 24 and lost at 4096 x 64
-    // (5.65 vs 5.05 ms per 1000) and 65536 x 256 (200 vs 82 ms per 200)
-    a.mid_max_cols = mvm_env_int("MVM_LSAP_MID_MAX_COLS", 0);
+    // one workgroup per problem: 256 threads (8 batched columns per thread) up to
+    // MVM_LSAP_MID_MAX_COLS long-side columns, 1024 threads (4 per thread) above.
+    // MI355X: 4096 x 64 problems 4.00 vs 4.36 ms per 1000 with 256 threads;
+    // 65536 x 256: 52 vs 80 ms per 200 with 1024 (tools/tune_lsap.py)
+    a.mid_max_cols = mvm_env_int("MVM_LSAP_MID_MAX_COLS", 8192);
     lsap_kernel<256><<<dim3((unsigned)n_problems), dim3(256), 0, s>>>(a);
     lsap_kernel<kLsapThreads><<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");

@@ -16,6 +16,7 @@ ENV = {"wg256": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "1000000"},
        "wg1024": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "0"},
        "multi": {"MVM_LSAP_MULTI_G": "-1"},
        "wave": {"MVM_LSAP_WAVE_MAX_COLS": "1024"},
+       "wave_wg256": {"MVM_LSAP_WAVE_MAX_COLS": "0", "MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "1000000"},
        "nowave": {"MVM_LSAP_WAVE_MAX_COLS": "0", "MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "0"}}
 KEYS = ("MVM_LSAP_MULTI_G", "MVM_LSAP_MID_MAX_COLS", "MVM_LSAP_WAVE_MAX_COLS")
 dev = torch.device("cuda", 0)
