@@ -620,7 +620,10 @@ __device__ bool group_barrier(SyncBlock *sb, unsigned int target) {
     __shared__ int s_ok;
     __syncthreads();
     if (threadIdx.x == 0) {
-        __threadfence();                                   // release this workgroup's writes
+        // agent-scope release (L2 write-back) then arrive; after the wait an
+        // agent-scope acquire (this CU's L1 invalidated): one of each, not two
+        // full __threadfence()s
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         atomicAdd(&sb->counter, 1u);
         int ok = 1;
         for (long spins = 0;; ++spins) {
@@ -635,7 +638,7 @@ __device__ bool group_barrier(SyncBlock *sb, unsigned int target) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        __threadfence();                                   // acquire the others' writes
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_ok = ok;
     }
     __syncthreads();
