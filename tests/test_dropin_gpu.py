@@ -169,6 +169,41 @@ def test_full_c2_cube_slice_bit_exact(cuda):
     assert np.array_equal(a.cpu().numpy(), ra)
 
 
+def test_full_c2_cube_properties(cuda):
+    """Config 2 cube at full size: 1000 scenes x 256^3 = 1.68e10 triples in the
+    bench's four 250-scene launches.  Size-independent properties on every
+    launch (the kernel's argmin/min equal the min over its own cube rows, with
+    the first-index rule), and bit-exact cubes vs the oracle on one scene per
+    launch."""
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(1000, 3, 256, seed=2024)
+    cube = torch.empty(250 * 256 ** 3, dtype=torch.float32, device=cuda)
+    for launch in range(4):
+        s0 = 250 * launch
+        co = b.cam_offs[3 * s0:3 * (s0 + 250) + 1]
+        pts = b.pts[int(co[0]):int(co[-1])]
+        co = co - co[0]
+        F = b.F[3 * s0:3 * (s0 + 250)]
+        plan = ops.TripletPlan(co, 250, device=cuda)
+        amin = torch.empty(plan.n_rows, dtype=torch.int32, device=cuda)
+        mval = torch.empty(plan.n_rows, dtype=torch.float32, device=cuda)
+        ops.triplet_cost_argmin(torch.from_numpy(pts).to(cuda), torch.from_numpy(co).to(cuda),
+                                torch.from_numpy(F).to(cuda), plan, out=(cube, amin, mval))
+        rows = cube.view(-1, 256)
+        mins = rows.min(dim=1).values
+        assert torch.equal(mins.view(torch.int32), mval.view(torch.int32))
+        first = (rows == mins[:, None]).int().argmax(dim=1).to(torch.int32)
+        assert torch.equal(first, amin)
+        k = 17 + launch                          # one scene per launch against the oracle
+        ck = co[3 * k:3 * k + 4]
+        rc, ra, _, _, _ = O.cube(pts[int(ck[0]):int(ck[-1])], ck - ck[0], F[3 * k:3 * k + 3], 1)
+        got = cube[k * 256 ** 3:(k + 1) * 256 ** 3].cpu().numpy()
+        assert np.array_equal(got.view(np.int32), rc.view(np.int32))
+        assert np.array_equal(amin[k * 65536:(k + 1) * 65536].cpu().numpy(), ra)
+        del rows, mins, first
+
+
 class _StubBoxes:
     def __init__(self, xyxy, conf, cls, dev):
         self.xyxy = torch.from_numpy(np.ascontiguousarray(xyxy, np.float32)).to(dev)
