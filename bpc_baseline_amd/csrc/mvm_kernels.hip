@@ -207,6 +207,7 @@ struct PairArgs {
     int32_t rows_per_wg;        // kWaves * RPW * row groups
     int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
     int32_t lane_results;       // 1: one RPW-lane store per group; 0: one store per row
+    int32_t xcd_remap;          // 1: each XCD takes a contiguous range of the logical grid
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -343,8 +344,16 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
     const int lane = t % kWave;
-    const int rb = (int)(blockIdx.x % (uint32_t)args.row_blocks);
-    const int sp = (int)(blockIdx.x / (uint32_t)args.row_blocks);
+    // dispatch places workgroup b on XCD b % 8; with xcd_remap each XCD walks a
+    // contiguous range of (scene, pair, row block)s, so a (scene, pair)'s row
+    // blocks share one L2 and its output region stays contiguous per XCD
+    uint32_t blk = blockIdx.x;
+    if (args.xcd_remap) {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const int rb = (int)(blk % (uint32_t)args.row_blocks);
+    const int sp = (int)(blk / (uint32_t)args.row_blocks);
     const int s = sp / args.n_pairs;
     const int p = sp - s * args.n_pairs;
     const int cam_a = args.pair_a[p], cam_b = args.pair_b[p];
@@ -951,6 +960,7 @@ struct CubeFusedArgs {
     int32_t *argmin;
     float *minval;
     int32_t j_blocks, i_blocks;
+    int32_t xcd_remap;          // as PairArgs::xcd_remap
 };
 
 struct LineRec {
@@ -981,9 +991,14 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
     const int lane = t % kWave;
+    uint32_t blk = blockIdx.x;
+    if (args.xcd_remap) {       // each XCD walks a contiguous range of tiles
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
     const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
-    const int s = (int)(blockIdx.x / per_scene);
-    const int rem = (int)(blockIdx.x % per_scene);
+    const int s = (int)(blk / per_scene);
+    const int rem = (int)(blk % per_scene);
     const int jb = rem % args.j_blocks;
     const int ib = rem / args.j_blocks;
     const int64_t *co = args.cam_offs + 3 * (int64_t)s;
@@ -1449,6 +1464,7 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
                          int row_groups, bool argmin, bool f64, hipStream_t stream) {
     a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
     a.lane_results = env_int("MVM_PAIRWISE_LANE_RESULTS", 1);
+    a.xcd_remap = env_int("MVM_PAIRWISE_XCD", 1);   // MI355X C3: 4.63 vs 4.72 ms per launch
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
@@ -1714,6 +1730,7 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
         c.cube = cube_dev;
         c.argmin = argmin_dev;
         c.minval = minval_dev;
+        c.xcd_remap = env_int("MVM_TRIPLET_XCD", 0);
         // MVM_TRIPLET_TILE: 3 = 16 i x 32 j (default), 4 = 32 i x 32 j, 2 = 8 i x 32 j, 0 = 16 i x 16 j
         const int tile = env_int("MVM_TRIPLET_TILE", 3);
         const int ib = tile == 4 ? 32 : (tile == 2 ? 8 : 16);

@@ -20,6 +20,7 @@ out = (torch.empty(plan.n_cube, dtype=torch.float32, device=dev),
 nbytes = 4.0 * plan.n_cube + 8.0 * plan.n_rows + 16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0]
 env = {"tile": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "0"},
        "fused": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1"},
+       "fusedx": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_XCD": "1"},
        "f32x32": {"MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_TILE": "4"},
        "f8x32": {"MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_TILE": "2"},
        "f16x16": {"MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_TILE": "0"},
@@ -40,7 +41,7 @@ ref = None
 for rnd in range(args.rounds + 1):
     for v in times:
         for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_VARIANT", "MVM_TRIPLET_TILE", "MVM_TRIPLET_SMALL",
-                  "MVM_TRIPLET_SMALL_IB", "MVM_TRIPLET_FUSED"):
+                  "MVM_TRIPLET_SMALL_IB", "MVM_TRIPLET_FUSED", "MVM_TRIPLET_XCD"):
             os.environ.pop(k, None)
         os.environ.update(env[v])
         ops.triplet_cost_argmin(pts, co, F, plan, out=out)
