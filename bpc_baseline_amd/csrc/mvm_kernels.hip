@@ -208,6 +208,7 @@ struct PairArgs {
     int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
     int32_t lane_results;       // 1: one RPW-lane store per group; 0: one store per row
     int32_t xcd_remap;          // 1: each XCD takes a contiguous range of the logical grid
+    int32_t interleave;         // 1: a matrix's row blocks interleave in units of 4*RPW rows
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -361,8 +362,16 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     const int na = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_a + 1] - oa);
     const int64_t ob = args.cam_offs[(int64_t)s * args.n_cams + cam_b];
     const int nb = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_b + 1] - ob);
-    const int row0 = rb * args.rows_per_wg;
+    // rows of the workgroup: contiguous [row0, row0 + rows_per_wg), or with
+    // `interleave` units of U = 4*RPW rows dealt round-robin over the matrix's
+    // row blocks (at any time a matrix's workgroups write adjacent units)
+    constexpr int U = kWaves * RPW;
+    const bool ilv = args.interleave != 0;
+    const int row0 = ilv ? rb * U : rb * args.rows_per_wg;
     if (row0 >= na) return;   // uniform over the workgroup
+    auto grow_of = [&](int x) {   // local row index -> matrix row
+        return ilv ? ((x / U) * args.row_blocks + rb) * U + (x % U) : row0 + x;
+    };
 
     double f[9];
 #pragma unroll
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     // every global load of the workgroup's rows happens here, before the first
     // store (on CDNA vmcnt orders loads behind earlier stores)
     for (int x = t; x < args.rows_per_wg; x += kThreads) {
-        const int i = row0 + x;
+        const int i = grow_of(x);
         const f64x2 v = (i < na) ? *reinterpret_cast<const f64x2 *>(args.pts + 2 * (oa + i))
                                  : f64x2{0.0, 0.0};
         *reinterpret_cast<f64x2 *>(s_rpt + 2 * x) = v;
@@ -404,18 +413,19 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     if (n_tiles == 1) load_tile(0);
     __syncthreads();
 
-    const int wg_rows = min(args.rows_per_wg, na - row0);
-    const int n_groups = (wg_rows + kWaves * RPW - 1) / (kWaves * RPW);   // uniform over the WG
+    const int n_groups = ilv ? min(args.rows_per_wg / U,
+                                   (na - row0 + args.row_blocks * U - 1) / (args.row_blocks * U))
+                             : (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
     for (int g = 0; g < n_groups; ++g) {
-        const int grow0 = row0 + (g * kWaves + wave) * RPW;   // this wave's first row
-        const int nrows = min(RPW, min(na, row0 + wg_rows) - grow0);   // scalar, may be <= 0
+        const int xw = (g * kWaves + wave) * RPW;             // this wave's first local row
+        const int grow0 = grow_of(xw);                        // ... and matrix row
+        const int nrows = min(RPW, na - grow0);               // scalar, may be <= 0
         if (lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
-            const int i = grow0 + lane;
             double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
             bool deg = true;
             if (lane < nrows) {
-                x = s_rpt[2 * (i - row0)];
-                y = s_rpt[2 * (i - row0) + 1];
+                x = s_rpt[2 * (xw + lane)];
+                y = s_rpt[2 * (xw + lane) + 1];
                 deg = row_line(f, x, y, l0, l1, l2);
             }
             s_row[wave][lane][0] = l0;
@@ -1338,10 +1348,18 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
 // Speed-of-light reference for the roofline: every workgroup writes one
 // contiguous 16 KiB block with 16-byte nontemporal stores (4 per lane, each
 // wave instruction 1 KiB contiguous) -- the store form of the residual kernels.
-template <int PER_LANE, bool NT>
+template <int PER_LANE, bool NT, bool XCD = false, bool SCRAMBLE = false>
 __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_t n16, float val) {
     const f32x4 v = {val, val, val, val};
-    const size_t base = (size_t)blockIdx.x * (PER_LANE * kThreads) + threadIdx.x;
+    uint32_t blk = blockIdx.x;
+    if (XCD) {                  // each XCD writes a contiguous eighth
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        uint32_t k = blk / 8;
+        const uint32_t cnt = q + (x < r ? 1u : 0u);
+        if (SCRAMBLE) k = (uint32_t)(((uint64_t)k * 2654435761ull) % cnt);   // odd multiplier:
+        blk = x * q + min(x, r) + k;                                         // a permutation when gcd = 1
+    }
+    const size_t base = (size_t)blk * (PER_LANE * kThreads) + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < PER_LANE; ++k) {
         const size_t i = base + (size_t)k * kThreads;
@@ -1374,11 +1392,16 @@ __global__ __launch_bounds__(kThreads) void write_probe_pol_kernel(f32x4 *dst, s
 // of 4 KiB, wave w owns rows 16w..16w+15 and walks chunk-outer / row-inner
 // (consecutive stores of a wave are 4 KiB apart); ROWMAJOR = 1 walks each
 // row's 4 chunks first (consecutive stores contiguous)
-template <bool ROWMAJOR>
+template <bool ROWMAJOR, bool XCD = false>
 __global__ __launch_bounds__(kThreads) void write_probe_rows_kernel(f32x4 *dst, size_t n16, float val) {
     const f32x4 v = {val, val, val, val};
     const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
-    const size_t base = (size_t)blockIdx.x * (64 * 256);         // 16-byte units: 64 rows x 256
+    uint32_t blk = blockIdx.x;
+    if (XCD) {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const size_t base = (size_t)blk * (64 * 256);         // 16-byte units: 64 rows x 256
     for (int a = 0; a < 16; ++a) {
         for (int b = 0; b < 4; ++b) {
             const int row = wave * 16 + (ROWMAJOR ? a : (a % 4) * 4 + b) ;
@@ -1465,6 +1488,7 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
     a.lane_results = env_int("MVM_PAIRWISE_LANE_RESULTS", 1);
     a.xcd_remap = env_int("MVM_PAIRWISE_XCD", 1);   // MI355X C3: 4.63 vs 4.72 ms per launch
+    a.interleave = env_int("MVM_PAIRWISE_INTERLEAVE", 0);
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
@@ -1658,6 +1682,13 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         case 6: write_probe_pol_kernel<1><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 7: write_probe_pol_kernel<2><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 8: write_probe_pol_kernel<3><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 11: write_probe_kernel<4, true, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 12: write_probe_rows_kernel<false, true><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 13: write_probe_kernel<4, false, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 14: write_probe_kernel<4, true, true, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 15: write_probe_kernel<8, true, true><<<(unsigned)((n16 + 8 * kThreads - 1) / (8 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 16: write_probe_kernel<16, true, true><<<(unsigned)((n16 + 16 * kThreads - 1) / (16 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 17: write_probe_kernel<2, true, true><<<(unsigned)((n16 + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 9: write_probe_rows_kernel<false><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 10: write_probe_rows_kernel<true><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
         default: write_probe_kernel<4, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
