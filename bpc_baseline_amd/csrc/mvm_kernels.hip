@@ -1665,7 +1665,9 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
     // 1 plain 16 KiB/WG, 2 nt 64 KiB/WG, 3 plain 64 KiB/WG, 4 nt grid-stride, 5 plain grid-stride,
     // 6 sc1, 7 sc0 sc1, 8 nt sc1 (16 KiB/WG), 9 / 10 the pairwise kernel's row order
     // (chunk-outer / row-major) on 256 KiB per WG
-    const int mode = env_int("MVM_PROBE_MODE", 0);
+    // default 17: the fastest store stream measured on MI355X (XCD-sequential
+    // 8 KiB blocks, 6.7 TB/s) -- the achievable ceiling bench.py reports
+    const int mode = env_int("MVM_PROBE_MODE", 17);
     const int per = (mode == 2 || mode == 3) ? 16 : 4;
     const size_t blocks = (n16 + per * kThreads - 1) / (per * kThreads);
     if (blocks == 0) return MVM_OK;

@@ -193,9 +193,11 @@ int mvm_select_triangulate(const float *cube_dev, const int64_t *cube_offs_dev,
 
 /*
  * Diagnostic: fill `bytes` (multiple of 16, 16-byte aligned) of device memory
- * with the same 16-byte nontemporal store stream the residual kernels use.
- * bench.py times it to report the achievable HBM write bandwidth next to the
- * kernels' roofline fraction.
+ * with the fastest 16-byte nontemporal store stream measured on MI355X: 8 KiB
+ * per workgroup, workgroups remapped so each XCD writes its own contiguous
+ * eighth in order.  bench.py times it to report the achievable HBM write
+ * bandwidth next to the kernels' roofline fraction (MVM_PROBE_MODE selects
+ * the other patterns studied in DESIGN.md §3.5).
  */
 int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream);
 

@@ -16,7 +16,7 @@ def one():
     e1.record()
     torch.cuda.synchronize()
     t = e0.elapsed_time(e1) / 10 * 1e-3
-    print(json.dumps({"mode": os.environ.get("MVM_PROBE_MODE", "0"), "grid": os.environ.get("MVM_PROBE_GRID", ""),
+    print(json.dumps({"mode": os.environ.get("MVM_PROBE_MODE", "17"), "grid": os.environ.get("MVM_PROBE_GRID", ""),
                       "TB/s": buf.numel() * 4 / t / 1e12}))
 
 if __name__ == "__main__":
