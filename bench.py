@@ -297,7 +297,16 @@ def main():
         ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
         parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rd.size} pairs)"
     elif env.is_root:
-        parity = "see tests/test_gpu_parity.py"
+        from oracle import oracle as O
+        c = chunks[-1]          # its cube is still in dist_buf
+        s_first = c.s0
+        co = batch.cam_offs[s_first * 3:(s_first + 1) * 3 + 1]
+        rc, ra, _, _, _ = O.cube(batch.pts[int(co[0]):int(co[-1])], co - co[0],
+                                 batch.F[s_first * 3:(s_first + 1) * 3], 1)
+        gc = dist_buf[:rc.size].cpu().numpy()
+        ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
+        ok = np.array_equal(gc.view(np.int32), rc.view(np.int32)) and np.array_equal(ga, ra)
+        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rc.size} triples)"
 
     # ---- PCIe-inclusive rate of one launch (never `value`) ------------------
     # the same launch fed from pinned host buffers: H2D of centroids, offsets
