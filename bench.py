@@ -156,8 +156,22 @@ def cpu_baseline(batch, mode: str, target_s: float):
     n1 = int(min(batch.n_scenes, max(1, round(target_s / 4 / max(per_scene * threads, 1e-9)))))
     u1, s1 = run(n1, 1)
     unit = "pairs/s" if mode == "pairwise" else "triples/s"
+    extra = {}
+    if mode == "pairwise":
+        # the vectorised NumPy restatement, one process, ~2 s sample
+        from oracle import numpy_port as NP
+        t0 = time.perf_counter()
+        NP.pairwise(batch.pts, batch.cam_offs, batch.F, batch.pairs, 1, C)
+        per = time.perf_counter() - t0
+        nn = int(min(batch.n_scenes, max(1, round(min(2.0, target_s / 4) / max(per, 1e-9)))))
+        t0 = time.perf_counter()
+        dn, _ = NP.pairwise(batch.pts, batch.cam_offs, batch.F, batch.pairs, nn, C)
+        sn = time.perf_counter() - t0
+        extra = {"numpy_value": dn.size / sn,
+                 "numpy_sample": f"{nn} scenes in {sn:.1f} s, oracle/numpy_port.py (vectorised NumPy, "
+                                 f"one process; no FMA, so a timing baseline)"}
     return {"value": units / secs, "unit": unit, "cores": threads, "kind": "port",
-            "one_core_value": u1 / s1, "one_core_sample": f"{n1} scenes in {s1:.1f} s",
+            "one_core_value": u1 / s1, "one_core_sample": f"{n1} scenes in {s1:.1f} s", **extra,
             "sample": f"{n_sc} scenes ({units:.3g} {unit[:-2]}) of this workload in {secs:.1f} s, "
                       f"oracle/mvm_oracle.c fp64 restatement (bit-exact to the reference), "
                       f"OpenMP x{threads} on {cpu_model()}"}

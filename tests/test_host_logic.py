@@ -219,3 +219,17 @@ def test_capture_cameras_equals_per_capture(tmp_path, capsys):
             assert np.array_equal(Ks[s, c], params[cam]["K"][im]) and Ks.dtype == np.float32
             ref = calc_pose_matrix(params[cam]["R"][im], params[cam]["t"][im])
             assert np.array_equal(RTs[s, c], ref) and RTs.dtype == ref.dtype
+
+
+def test_numpy_port_agrees_in_float32():
+    """The vectorised NumPy restatement (bench.py's numpy CPU baseline) has no
+    FMA, so only float32 agreement with the bit-exact C oracle is expected."""
+    from bpc_baseline_amd.synth import make_scenes
+    from oracle import numpy_port as NP
+    from oracle import oracle as O
+    b = make_scenes(4, 4, 120, seed=5)
+    d, a = NP.pairwise(b.pts, b.cam_offs, b.F, b.pairs, 4, 4)
+    rd, ra, _, _, _ = O.pairwise(b.pts, b.cam_offs, b.F, b.pairs, 4, 4)
+    assert d.size == rd.size > 300000
+    assert np.mean(d.view(np.int32) == rd.view(np.int32)) > 0.9999
+    assert np.mean(a == ra) > 0.999
