@@ -170,6 +170,24 @@ def cpu_baseline(batch, mode: str, target_s: float):
         extra = {"numpy_value": dn.size / sn,
                  "numpy_sample": f"{nn} scenes in {sn:.1f} s, oracle/numpy_port.py (vectorised NumPy, "
                                  f"one process; no FMA, so a timing baseline)"}
+    # the reference's own cost model: one small-array NumPy evaluation per pair
+    # in Python loops (oracle/reference_loop.py, bit-exact to the reference)
+    from oracle import reference_loop as RL
+    co = batch.cam_offs
+    if mode == "pairwise":
+        a, b = batch.pairs[0]
+        n_ref, s_ref = RL.pairs_per_second(batch.pts[co[a]:co[a + 1]], batch.pts[co[b]:co[b + 1]],
+                                           batch.F[0], seconds=2.0)
+    else:
+        views = [batch.pts[co[v]:co[v + 1]][:8] for v in range(3)]
+        Fs = [np.asarray(batch.F[q], np.float64).reshape(3, 3) for q in range(3)]
+        n_ref, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 2.0:
+            n_ref += RL.cube(*views, *Fs).size
+        s_ref = time.perf_counter() - t0
+    extra["reference_loop_value"] = n_ref / s_ref if s_ref else None
+    extra["reference_loop_sample"] = (f"{n_ref} {unit[:-2]} in {s_ref:.1f} s, oracle/reference_loop.py "
+                                      "(the reference's per-pair NumPy calls in Python loops, one core)")
     return {"value": units / secs, "unit": unit, "cores": threads, "kind": "port",
             "one_core_value": u1 / s1, "one_core_sample": f"{n1} scenes in {s1:.1f} s", **extra,
             "sample": f"{n_sc} scenes ({units:.3g} {unit[:-2]}) of this workload in {secs:.1f} s, "

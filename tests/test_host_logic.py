@@ -233,3 +233,18 @@ def test_numpy_port_agrees_in_float32():
     assert d.size == rd.size > 300000
     assert np.mean(d.view(np.int32) == rd.view(np.int32)) > 0.9999
     assert np.mean(a == ra) > 0.999
+
+
+def test_reference_loop_restatement_is_bit_exact(golden):
+    """oracle/reference_loop.py (the reference's per-pair NumPy cost model, timed
+    by bench.py) reproduces the reference's own outputs bit for bit."""
+    from oracle import reference_loop as RL
+    z = golden("a1_epipolar_error.npz")
+    got = np.array([RL.residual(z["p1"][k], z["p2"][k], np.asarray(z["F"][k]).reshape(3, 3))
+                    for k in range(len(z["e"]))])
+    assert np.array_equal(got.view(np.int64), np.asarray(z["e"], np.float64).view(np.int64))
+    g = golden("a3_cost_cubes.npz")
+    for n in ("c4", "c537", "degen", "dup"):
+        F12, F13, F23 = (np.asarray(f, np.float64).reshape(3, 3) for f in g[f"{n}_F"])
+        c = RL.cube(g[f"{n}_p1"], g[f"{n}_p2"], g[f"{n}_p3"], F12, F13, F23)
+        assert np.array_equal(c.view(np.int32), g[f"{n}_cube"].view(np.int32)), n
