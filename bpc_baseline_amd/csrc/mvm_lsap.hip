@@ -54,6 +54,7 @@ struct LsapArgs {
     int32_t multi_g;            // > 1: larger problems run in lsap_multi_kernel, G workgroups each
     int32_t mid_max_cols;       // long sides in (wave_max_cols, this]: 256-thread lsap_kernel
     unsigned char *sync;        // per-problem barrier + reduction slots (multi kernel)
+    int32_t dpp;                // 1: DPP wave reductions in lsap_wave_kernel
 };
 
 struct Red {
@@ -80,6 +81,45 @@ __device__ __forceinline__ Red red_wave(Red r) {
         r = red_combine(r, o);
     }
     return r;
+}
+
+// The same reduction with DPP: four row-local steps (quad_perm [1,0,3,2],
+// quad_perm [2,3,0,1], row_half_mirror, row_mirror) leave every lane of a
+// 16-lane row with the row's result; the four rows are then combined on the
+// scalar unit from v_readlane.  No LDS round trips (a shuffle is a bpermute).
+template <int CTRL>
+__device__ __forceinline__ Red red_dpp_step(Red r) {
+    const uint64_t mb = (uint64_t)__double_as_longlong(r.m);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)mb, (int)(uint32_t)mb, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(mb >> 32), (int)(uint32_t)(mb >> 32), CTRL,
+                                               0xF, 0xF, false);
+    Red o;
+    o.m = __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+    o.first = __builtin_amdgcn_update_dpp(r.first, r.first, CTRL, 0xF, 0xF, false);
+    o.last_free = __builtin_amdgcn_update_dpp(r.last_free, r.last_free, CTRL, 0xF, 0xF, false);
+    return red_combine(r, o);
+}
+
+__device__ __forceinline__ Red red_readlane(const Red &r, int l) {
+    const uint64_t mb = (uint64_t)__double_as_longlong(r.m);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mb, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mb >> 32), l);
+    Red o;
+    o.m = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+    o.first = __builtin_amdgcn_readlane(r.first, l);
+    o.last_free = __builtin_amdgcn_readlane(r.last_free, l);
+    return o;
+}
+
+__device__ __forceinline__ Red red_wave_dpp(Red r) {
+    r = red_dpp_step<0xB1>(r);
+    r = red_dpp_step<0x4E>(r);
+    r = red_dpp_step<0x141>(r);
+    r = red_dpp_step<0x140>(r);
+    Red a = red_readlane(r, 0);
+    a = red_combine(a, red_readlane(r, 16));
+    a = red_combine(a, red_readlane(r, 32));
+    return red_combine(a, red_readlane(r, 48));
 }
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -259,7 +299,7 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
                     }
                 }
             }
-            best = red_wave(best);
+            best = a.dpp ? red_wave_dpp(best) : red_wave(best);
             if (lane == 0) s_red[wave] = best;
             __syncthreads();
             if (t == 0) {
@@ -449,7 +489,7 @@ __device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_
                     if (free_col) best.last_free = max(best.last_free, pos[q]);
                 }
             }
-            best = red_wave(best);
+            best = a.dpp ? red_wave_dpp(best) : red_wave(best);
             if (!(best.m < INFINITY)) {
                 if (lane == 0) a.status[p] = 2;   // infeasible
                 return;
@@ -936,6 +976,7 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
                    ~(uintptr_t)255)};   // at or after the per-problem regions (all 256-aligned)
+    a.dpp = mvm_env_int("MVM_LSAP_DPP", 1);   // DPP wave reductions (0: shuffles)
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (wave_max > 0) {
         const dim3 grid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
