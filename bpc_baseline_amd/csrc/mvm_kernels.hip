@@ -1412,6 +1412,27 @@ __global__ __launch_bounds__(kThreads) void write_probe_rows_kernel(f32x4 *dst, 
     }
 }
 
+// model of a "16-row unit" decomposition: a persistent grid, workgroup k of
+// XCD x walks units k, k+W, ... of that XCD's eighth; per unit it reads a
+// 44 KiB line block (from a 4 MiB L2-resident region) and writes 64 KiB
+// (16 rows of 4 KiB, 4 waves x 4 rows)
+__global__ __launch_bounds__(kThreads) void write_probe_units_kernel(f32x4 *dst, size_t n16,
+                                                                     const f32x4 *lines) {
+    const uint32_t W = gridDim.x / 8, x = blockIdx.x % 8, k = blockIdx.x / 8;
+    const size_t n_units = n16 / 4096;                        // 64 KiB = 4096 x 16 B
+    const size_t u0 = n_units * x / 8, u1 = n_units * (x + 1) / 8;
+    const int t = threadIdx.x;
+    for (size_t u = u0 + k; u < u1; u += W) {
+        const f32x4 *lb = lines + (u % 90) * 2816;            // 44 KiB = 2816 x 16 B
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 11; ++q) acc += lb[t + 256 * q];
+        f32x4 *ob = dst + u * 4096;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) __builtin_nontemporal_store(acc, ob + t + 256 * q);
+    }
+}
+
 // grid-stride variant: a fixed grid of `waves per CU` x 256 CUs workgroups
 template <bool NT>
 __global__ __launch_bounds__(kThreads) void write_probe_stride_kernel(f32x4 *dst, size_t n16,
@@ -1691,6 +1712,14 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         case 15: write_probe_kernel<8, true, true><<<(unsigned)((n16 + 8 * kThreads - 1) / (8 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 16: write_probe_kernel<16, true, true><<<(unsigned)((n16 + 16 * kThreads - 1) / (16 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 17: write_probe_kernel<2, true, true><<<(unsigned)((n16 + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 18: {
+            // lines region: the last 4 MiB of the buffer (units stop before it)
+            const size_t reserve = (4u << 20) / 16;
+            if (n16 <= reserve + 4096) return fail(MVM_ERR_INVALID_ARGUMENT, "buffer too small");
+            const unsigned grid = (unsigned)env_int("MVM_PROBE_GRID", 8 * 96);
+            write_probe_units_kernel<<<grid, kThreads, 0, s>>>(d, n16 - reserve, d + (n16 - reserve));
+            break;
+        }
         case 9: write_probe_rows_kernel<false><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 10: write_probe_rows_kernel<true><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
         default: write_probe_kernel<4, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
