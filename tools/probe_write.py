@@ -24,7 +24,7 @@ if __name__ == "__main__":
         one()
     else:
         modes = [(0, ""), (1, ""), (2, ""), (3, ""), (4, "1024"), (4, "2048"), (4, "4096"),
-                 (5, "2048"), (5, "4096"), (6, ""), (7, ""), (8, ""), (9, ""), (10, ""), (11, ""), (12, ""), (13, ""), (14, ""), (15, ""), (16, ""), (17, ""), (18, "512"), (18, "768"), (18, "1024"), (18, "1536")]
+                 (5, "2048"), (5, "4096"), (6, ""), (7, ""), (8, ""), (9, ""), (10, ""), (11, ""), (12, ""), (13, ""), (14, ""), (15, ""), (16, ""), (17, ""), (18, "512"), (18, "768"), (18, "1024"), (18, "1536"), (18, "65472")]
         if len(sys.argv) > 1:
             keep = set(int(x) for x in sys.argv[1].split(","))
             modes = [m for m in modes if m[0] in keep]
