@@ -15,7 +15,8 @@ with every O(n) and larger step on the GPU:
   5. mvm_select_triangulate   cost < threshold, stable sort by cost, DLT
 
 The only device->host transfer before the results is the per-image kept
-count (n_img int32), which sizes the cube and assignment layouts.
+count (n_img int32, with the packing status), which sizes the cube and
+assignment layouts; the results need one more (statuses + match counts).
 
 Results equal, capture by capture, the reference's ``_match`` outputs fed with
 ``_detect``'s detections: match indices and order exactly, ``t`` to rounding
@@ -117,8 +118,10 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev) if proj is None else proj
     mark("F+P host")
 
-    counts_host = counts.cpu().numpy().astype(np.int64)
-    if int(status.item()) != 0:
+    # one device -> host copy: the kept counts and the packing status
+    ch = torch.cat([counts, status]).cpu().numpy().astype(np.int64)
+    counts_host = ch[:-1]
+    if ch[-1] != 0:
         raise ValueError("detector box with a non-finite or out-of-range coordinate")
     cam_offs_host = np.zeros(n_img + 1, np.int64)
     np.cumsum(counts_host, out=cam_offs_host[1:])
@@ -138,11 +141,12 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                                                    row_ind, col_ind, pts, proj_dev,
                                                    float(matching_threshold))
     mark("select")
-    bad = lstat.cpu().numpy()
+    # one device -> host copy: assignment statuses and match counts
+    sc = torch.cat([lstat, count]).cpu().numpy()
+    bad, count_h = sc[:S], sc[S:]
     if np.any(bad):
         raise ValueError(f"assignment failed for captures {np.nonzero(bad)[0][:8].tolist()} "
                          "(cost matrix contains invalid numeric entries or is infeasible)")
-    count_h = count.cpu().numpy()
     mark("results D2H")
     return MatchBatch(match=match, cost=cost, X=X, count=count_h,
                       offs=lplan.out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
