@@ -668,148 +668,8 @@ __device__ __forceinline__ bool third_fast_ok(double q0) {
     return !near_mid && in_range;                                  // NaN/inf/negative: false
 }
 
-// Three-camera cube for views with P <= 256 (one k chunk): lanes own 4
-// consecutive k; each wave owns RPW consecutive j and keeps e23[j][k] for
-// them in registers (8*RPW VGPRs), then sweeps i: e13[i][k] is one 32-byte
-// load per lane per i, e12[i][j] a scalar load, and every (i, j) row is one
-// 16-byte-per-lane coalesced store followed by a DPP argmin over k.
-// Workgroup = (scene, block of 4*RPW j's, slice of i).
-struct Cube256Args {
-    const int64_t *cam_offs;
-    const double *e;
-    int64_t mat_stride;
-    int64_t ld;
-    const int64_t *cube_offs;
-    const int64_t *row_offs;
-    float *cube;
-    int32_t *argmin;
-    float *minval;
-    int32_t j_blocks, i_splits, i_chunk;
-};
-
-// Sweep i in [i_begin, i_end) for RPW rows j0.. of one scene.  FULL: P == 256
-// and the cube rows are 16-byte aligned, so every lane owns 4 valid k and all
-// loads/stores are unconditional vectors.
-template <int RPW, bool FULL>
-__device__ __forceinline__ void triplet_rows(const Cube256Args &args, const double *e12,
-                                             const double *e13, const double *e23, int M, int P,
-                                             int j0, int nrows, int i_begin, int i_end,
-                                             int64_t coff, int64_t roff, int lane) {
-    const int kb = kColsPerLane * lane;
-    const int kvalid = FULL ? kColsPerLane : P - kb;
-    double a23[RPW][kColsPerLane];
-#pragma unroll
-    for (int r = 0; r < RPW; ++r)
-        load4(e23 + (int64_t)(j0 + min(r, nrows - 1)) * args.ld + kb, kvalid, a23[r]);
-
-    // software pipeline: e13 row and e12 slice of i+1 are loaded during row i
-    double n13[kColsPerLane], n12[RPW];
-    auto fetch = [&](int i) {
-        load4(e13 + (int64_t)i * args.ld + kb, kvalid, n13);
-#pragma unroll
-        for (int r = 0; r < RPW; r += 2) {
-            const f64x2 v2 = *reinterpret_cast<const f64x2 *>(e12 + (int64_t)i * args.ld + j0 + r);
-            n12[r] = v2.x;
-            n12[r + 1] = v2.y;
-        }
-    };
-    fetch(i_begin);
-    for (int i = i_begin; i < i_end; ++i) {
-        double a13[kColsPerLane], a12[RPW];
-#pragma unroll
-        for (int q = 0; q < kColsPerLane; ++q) a13[q] = n13[q];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) a12[r] = n12[r];
-        if (i + 1 < i_end) fetch(i + 1);
-
-        uint32_t key[RPW];
-        int32_t idx[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            key[r] = kKeyInvalid;
-            idx[r] = 0x7FFFFFFF;
-            if (r >= nrows) continue;   // uniform
-            double sum[kColsPerLane], q0[kColsPerLane];
-            bool ok = true;
-#pragma unroll
-            for (int q = 0; q < kColsPerLane; ++q) {
-                sum[q] = (a12[r] + a13[q]) + a23[r][q];       // (e12 + e13) + e23, :81
-                q0[q] = sum[q] * kThird;
-                ok &= third_fast_ok(q0[q]);
-            }
-            float v[kColsPerLane];
-            const int64_t row = (int64_t)i * M + j0 + r;
-            if (FULL && args.cube && __all(ok)) {   // finite, fast division exact
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                              (uint32_t)kb * 4u, v);
-                Best b{v[0], kb};
-#pragma unroll
-                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                key[r] = __float_as_uint(b.v) + 1u;
-                idx[r] = b.j;
-            } else {
-                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
-                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                    v[q] = (float)qq;
-                    if (q < kvalid) {
-                        if (args.cube)
-                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
-                        best_update_safe(b, v[q], kb + q);
-                    }
-                }
-                key[r] = best_key(b);
-                idx[r] = b.j;
-            }
-        }
-        uint32_t kmin[RPW];
-        int32_t imin[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) {   // independent DPP chains interleave
-            kmin[r] = kKeyInvalid;
-            imin[r] = 0;
-            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
-        }
-        store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
-                               roff + (int64_t)i * M + j0);
-    }
-}
-
-template <int RPW>
-__global__ __launch_bounds__(kThreads) void triplet256_kernel(Cube256Args args) {
-    const int t = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
-    const int lane = t % kWave;
-    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_splits);
-    const int s = (int)(blockIdx.x / per_scene);
-    const int rem = (int)(blockIdx.x % per_scene);
-    const int jb = rem % args.j_blocks;
-    const int is = rem / args.j_blocks;
-    const int64_t c0 = args.cam_offs[3 * (int64_t)s];
-    const int N = (int)(args.cam_offs[3 * (int64_t)s + 1] - c0);
-    const int M = (int)(args.cam_offs[3 * (int64_t)s + 2] - args.cam_offs[3 * (int64_t)s + 1]);
-    const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
-    const int j0 = (jb * kWaves + wave) * RPW;
-    const int i_begin = is * args.i_chunk;
-    const int i_end = min(N, i_begin + args.i_chunk);
-    if (j0 >= M || i_begin >= N || P == 0) return;   // wave-uniform; no barriers below
-    const int nrows = min(RPW, M - j0);
-    const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
-    const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride;
-    const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
-    const int64_t coff = args.cube_offs[s];
-    const int64_t roff = args.row_offs[s];
-    if (P == kChunk && (coff & 3) == 0)
-        triplet_rows<RPW, true>(args, e12, e13, e23, M, P, j0, nrows, i_begin, i_end, coff, roff, lane);
-    else
-        triplet_rows<RPW, false>(args, e12, e13, e23, M, P, j0, nrows, i_begin, i_end, coff, roff, lane);
-}
-
 // ------------------------------------------- tiled triplet kernel (v3) ----
-// Same arithmetic as triplet256_kernel, different schedule: a workgroup owns
+// The 3-camera cube for P <= 256 from the fp64 workspace: a workgroup owns
 // (scene, 16 consecutive j, IB consecutive i).  Its prologue loads everything
 // the tile needs -- e23 rows into registers, the e13[i-block][:] and
 // e12[i-block][j-block] tiles into LDS -- with ONE wait; the main loop then
@@ -1454,7 +1314,6 @@ __global__ __launch_bounds__(kThreads) void write_probe_stride_kernel(f32x4 *dst
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;       // pairwise default: 64 rows per workgroup
 constexpr int kTripletRowsPerWave = 8; // generic triplet: 32 (i, j) rows per workgroup
-constexpr int kTriplet256RowsPerWave = 4;   // P <= 256 triplet: e23 rows held per wave
 
 int fail(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 int fail(int code, const char *fmt, ...);
@@ -1483,7 +1342,7 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 
 // Tuning knobs (read per launch; defaults tuned on MI355X):
 //   MVM_PAIRWISE_LANE_RESULTS  1: argmin rows stored by RPW lanes at once
-//   MVM_TRIPLET_RPW / MVM_TRIPLET_GENERIC  cube kernel variant
+//   MVM_TRIPLET_VARIANT  3: tiled/fused cube kernels (default), 1: generic
 //   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
 //   MVM_PAIRWISE_NT   row store policy: 1 nt (default), 0 default, 2 sc1, 3 sc0 sc1
@@ -1750,7 +1609,7 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     if (((uintptr_t)workspace_dev & 15) != 0)
         return fail(MVM_ERR_INVALID_ARGUMENT, "workspace not 16-byte aligned");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled, 2 register, 1 generic
+    const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled / fused, 1 generic
     if (max_n <= kSmallMaxN && env_int("MVM_TRIPLET_SMALL", 1) && variant == 3) {
         // one workgroup per scene, everything in LDS, no workspace pass
         CubeSmallArgs c{};
@@ -1849,37 +1708,6 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
         default: triplet_tile_kernel<16, 8><<<grid, block, 0, s>>>(c); break;
         }
         return check_launch("triplet_tile_kernel");
-    }
-    if (max_n <= kChunk && variant == 2) {
-        // every P <= 256: register-resident e23 kernel
-        const int rpw = env_int("MVM_TRIPLET_RPW", kTriplet256RowsPerWave) == 8 ? 8 : 4;
-        Cube256Args c{};
-        c.cam_offs = cam_offs_dev;
-        c.e = (const double *)workspace_dev;
-        c.mat_stride = mat_stride;
-        c.ld = ld;
-        c.cube_offs = cube_offs_dev;
-        c.row_offs = row_offs_dev;
-        c.cube = cube_dev;
-        c.argmin = argmin_dev;
-        c.minval = minval_dev;
-        c.j_blocks = (max_n + kWaves * rpw - 1) / (kWaves * rpw);
-        // split i so the grid has >= ~4096 workgroups (>= 16 per CU)
-        const int64_t base = (int64_t)n_scenes * c.j_blocks;
-        const int64_t want = (4096 + base - 1) / base;
-        const int64_t cap = max_n / 8 > 1 ? max_n / 8 : 1;
-        const int splits = (int)(want < 1 ? 1 : (want > cap ? cap : want));
-        c.i_chunk = (max_n + splits - 1) / splits;
-        c.i_splits = (max_n + c.i_chunk - 1) / c.i_chunk;
-        const int64_t blocks = base * c.i_splits;
-        if (blocks > 0x7FFFFFFFLL)
-            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
-                        (long long)blocks);
-        if (rpw == 4)
-            triplet256_kernel<4><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
-        else
-            triplet256_kernel<8><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
-        return check_launch("triplet256_kernel");
     }
     CubeArgs c{};
     c.cam_offs = cam_offs_dev;

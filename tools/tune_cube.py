@@ -8,7 +8,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=250)
 ap.add_argument("--dets", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="tile,rpw4,generic")
+ap.add_argument("--variants", default="fused,tile,generic")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 b = make_scenes(args.scenes, 3, args.dets, seed=0)
@@ -33,8 +33,6 @@ env = {"tile": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPL
        "t8x16": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "1"},
        "t8x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "2"},
        "t16x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "3"},
-       "rpw8": {"MVM_TRIPLET_VARIANT": "2", "MVM_TRIPLET_RPW": "8"},
-       "rpw4": {"MVM_TRIPLET_VARIANT": "2", "MVM_TRIPLET_RPW": "4"},
        "generic": {"MVM_TRIPLET_VARIANT": "1"}}
 times = {v: [] for v in args.variants.split(",")}
 ref = None
