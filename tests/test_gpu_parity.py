@@ -192,3 +192,45 @@ def test_deterministic_repeat(cuda):
     r2 = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 4, 4)
     for x, y in zip(r1, r2):
         assert np.array_equal(np.asarray(x).view(np.uint8), np.asarray(y).view(np.uint8))
+
+
+def test_launches_capture_into_a_hip_graph(cuda):
+    """The C ABI enqueues work only (no allocation, copy or sync inside), so a
+    step of launches can be captured into a hipGraph (torch.cuda.CUDAGraph on
+    ROCm) and replayed; replay reproduces the eager results bit for bit."""
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(6, 4, 200, seed=12)
+    c = make_scenes(4, 3, 40, seed=13)
+    pp = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=cuda)
+    tp = ops.TripletPlan(c.cam_offs, c.n_scenes, device=cuda)
+    t = lambda a: torch.from_numpy(a).to(cuda)
+    bp, bc, bF = t(b.pts), t(b.cam_offs), t(b.F)
+    cp, cc, cF = t(c.pts), t(c.cam_offs), t(c.F)
+    dist = torch.empty(pp.n_dist, dtype=torch.float32, device=cuda)
+    am = torch.empty(pp.n_rows, dtype=torch.int32, device=cuda)
+    mv = torch.empty(pp.n_rows, dtype=torch.float32, device=cuda)
+    cube = torch.empty(tp.n_cube, dtype=torch.float32, device=cuda)
+    cam = torch.empty(tp.n_rows, dtype=torch.int32, device=cuda)
+    cmv = torch.empty(tp.n_rows, dtype=torch.float32, device=cuda)
+
+    def step():
+        ops.pairwise_residual_argmin(bp, bc, bF, pp, out=(dist, am, mv))
+        ops.triplet_cost_argmin(cp, cc, cF, tp, out=(cube, cam, cmv))
+
+    s = torch.cuda.Stream(cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        step()                                   # warm-up on the side stream
+    torch.cuda.current_stream(cuda).wait_stream(s)
+    ref = [x.clone() for x in (dist, am, cube, cam)]
+    for x in (dist, am, cube, cam):
+        x.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    g.replay()
+    torch.cuda.synchronize(cuda)
+    for x, r in zip((dist, am, cube, cam), ref):
+        assert torch.equal(x.view(torch.int32) if x.dtype == torch.float32 else x,
+                           r.view(torch.int32) if r.dtype == torch.float32 else r)
