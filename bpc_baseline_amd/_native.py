@@ -58,6 +58,10 @@ SIGNATURES = {
     "mvm_lsap_solve": (ctypes.c_int, [
         _vp, _vp, _vp, _i32, _vp, _vp,      # cost, cost_offs, dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp, _vp]),     # workspace, bytes, row_ind, col_ind, status, stream
+    "mvm_lsap_solve_bounded": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _vp, _vp,
+        _vp, _sz, _vp, _vp, _vp,
+        _i64, _i64, _vp]),                  # long_min, long_max, stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
         ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id

@@ -579,7 +579,11 @@ __global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs 
     if (p >= n) return;
     const int64_t R = a.dims[2 * p], Kc = a.dims[2 * p + 1];
     const int64_t nc = R > Kc ? R : Kc;
-    if (R == 0 || Kc == 0 || nc > a.wave_max_cols) return;   // empty: lsap_kernel sets status
+    if (R == 0 || Kc == 0) {               // empty (every kernel class writes the same 0)
+        if (lane == 0) a.status[p] = 0;
+        return;
+    }
+    if (nc > a.wave_max_cols) return;
     // each instantiation owns the long sides (32K, 64K]: its own register budget
     if (nc > 64 * K || (K > 1 && nc <= 32 * K)) return;
     lsap_wave_solve<K>(a, p, R, Kc, s_u[wave], s_c4r[wave], lane);
@@ -956,6 +960,17 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
                    int32_t n_problems, const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
                    void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
                    int64_t *col_ind_dev, int32_t *status_dev, mvm_stream_t stream) {
+    return mvm_lsap_solve_bounded(cost_dev, cost_offs_dev, dims_dev, n_problems, ws_offs_dev,
+                                  out_offs_dev, workspace_dev, workspace_bytes, row_ind_dev,
+                                  col_ind_dev, status_dev, 1, INT64_MAX, stream);
+}
+
+int mvm_lsap_solve_bounded(const float *cost_dev, const int64_t *cost_offs_dev,
+                           const int64_t *dims_dev, int32_t n_problems,
+                           const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
+                           void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
+                           int64_t *col_ind_dev, int32_t *status_dev, int64_t long_min,
+                           int64_t long_max, mvm_stream_t stream) {
     mvm_clear_error();
     if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
     if (n_problems == 0) return MVM_OK;
@@ -978,15 +993,27 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
                    ~(uintptr_t)255)};   // at or after the per-problem regions (all 256-aligned)
     a.dpp = mvm_env_int("MVM_LSAP_DPP", 1);   // DPP wave reductions (0: shuffles)
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (wave_max > 0) {
-        const dim3 grid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
-        const dim3 block(64 * kWaveProblems);
-        lsap_wave_kernel<1><<<grid, block, 0, s>>>(a, n_problems);
-        if (wave_max > 64) lsap_wave_kernel<2><<<grid, block, 0, s>>>(a, n_problems);
-        if (wave_max > 128) lsap_wave_kernel<4><<<grid, block, 0, s>>>(a, n_problems);
-        if (wave_max > 256) lsap_wave_kernel<8><<<grid, block, 0, s>>>(a, n_problems);
-        if (wave_max > 512) lsap_wave_kernel<16><<<grid, block, 0, s>>>(a, n_problems);
+    // long_min / long_max bound max(rows, cols) over the non-empty problems
+    // (long_max 0: all empty): kernel classes that cannot have work are not
+    // launched.  Every class writes status 0 for empty problems.
+    if (long_max < 1) {
+        long_min = long_max = 0;
     }
+    auto overlaps = [&](int64_t lo, int64_t hi) { return long_max >= lo && long_min <= hi; };
+    const dim3 wgrid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
+    const dim3 wblock(64 * kWaveProblems);
+    bool empty_done = false;
+    if (wave_max > 0) {
+        if (overlaps(0, 64) || long_max == 0) {
+            lsap_wave_kernel<1><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
+        if (wave_max > 64 && overlaps(65, 128)) lsap_wave_kernel<2><<<wgrid, wblock, 0, s>>>(a, n_problems);
+        if (wave_max > 128 && overlaps(129, 256)) lsap_wave_kernel<4><<<wgrid, wblock, 0, s>>>(a, n_problems);
+        if (wave_max > 256 && overlaps(257, 512)) lsap_wave_kernel<8><<<wgrid, wblock, 0, s>>>(a, n_problems);
+        if (wave_max > 512 && overlaps(513, 1024)) lsap_wave_kernel<16><<<wgrid, wblock, 0, s>>>(a, n_problems);
+    }
+    const bool big = long_max > wave_max;   // anything left for the workgroup kernels
     // Few large problems: G co-resident workgroups per problem (cooperative
     // launch guarantees co-residency).  MVM_LSAP_MULTI_G: -1 auto (default),
     // 0/1 off, 2..16 forced.  Auto uses as many workgroups per problem as the
@@ -1006,7 +1033,7 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
     } else {
         G = 0;
     }
-    if (G >= 2) {
+    if (G >= 2 && big) {
         a.multi_g = G;
         if (hipMemsetAsync(a.sync, 0, sync_bytes, s) != hipSuccess)
             return mvm_fail(MVM_ERR_HIP, "hipMemsetAsync(lsap sync) failed");
@@ -1024,8 +1051,11 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
     // MI355X: 4096 x 64 problems 4.00 vs 4.36 ms per 1000 with 256 threads;
     // 65536 x 256: 52 vs 80 ms per 200 with 1024 (tools/tune_lsap.py)
     a.mid_max_cols = mvm_env_int("MVM_LSAP_MID_MAX_COLS", 8192);
-    lsap_kernel<256><<<dim3((unsigned)n_problems), dim3(256), 0, s>>>(a);
-    lsap_kernel<kLsapThreads><<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
+    const int64_t lo256 = (int64_t)wave_max + 1, hi256 = a.mid_max_cols;
+    if (!empty_done || (a.multi_g <= 1 && big && overlaps(lo256, hi256)))
+        lsap_kernel<256><<<dim3((unsigned)n_problems), dim3(256), 0, s>>>(a);
+    if (a.multi_g <= 1 && big && long_max > (hi256 > wave_max ? hi256 : (int64_t)wave_max))
+        lsap_kernel<kLsapThreads><<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");
 }
 

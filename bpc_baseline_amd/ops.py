@@ -141,7 +141,7 @@ def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minv
                          mutates_args=("workspace", "row_ind", "col_ind", "status"))
 def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
                    out_offs: Tensor, workspace: Tensor, row_ind: Tensor, col_ind: Tensor,
-                   status: Tensor) -> None:
+                   status: Tensor, long_min: int = 1, long_max: int = 2 ** 62) -> None:
     dev = cost.device
     if dev.type != "cuda":
         raise ValueError("cost must be a GPU tensor (the matcher has no CPU path)")
@@ -152,14 +152,16 @@ def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tenso
                      (status, "status", torch.int32)):
         _require(t, n, dt, dev)
     n = status.numel()
-    st = _native.load().mvm_lsap_solve(_p(cost), _p(cost_offs), _p(dims), n, _p(ws_offs),
-                                       _p(out_offs), _p(workspace), workspace.numel(),
-                                       _p(row_ind), _p(col_ind), _p(status), _stream(cost))
-    _native.check("mvm_lsap_solve", st)
+    st = _native.load().mvm_lsap_solve_bounded(_p(cost), _p(cost_offs), _p(dims), n, _p(ws_offs),
+                                               _p(out_offs), _p(workspace), workspace.numel(),
+                                               _p(row_ind), _p(col_ind), _p(status), long_min,
+                                               long_max, _stream(cost))
+    _native.check("mvm_lsap_solve_bounded", st)
 
 
 @lsap_solve_out.register_fake
-def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status):
+def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, long_min=1,
+      long_max=2 ** 62):
     return None
 
 
@@ -413,6 +415,9 @@ class LsapPlan:
         self.out_offs = torch.from_numpy(out_offs).to(self.device)
         self.workspace = torch.empty(max(int(total), 16), dtype=torch.uint8, device=self.device)
         self.n_out = int(out_offs[-1])
+        longs = np.maximum(rows, cols)[(rows > 0) & (cols > 0)]
+        self.long_min = int(longs.min()) if longs.size else 0     # bounds for the launch
+        self.long_max = int(longs.max()) if longs.size else 0
 
 
 def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan):
@@ -423,7 +428,8 @@ def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPla
     col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
-                                     plan.workspace, row_ind, col_ind, status)
+                                     plan.workspace, row_ind, col_ind, status, plan.long_min,
+                                     plan.long_max)
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
 
 

@@ -135,6 +135,18 @@ int mvm_lsap_solve(const float *cost_dev, const int64_t *cost_offs_dev, const in
                    int32_t n_problems, const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
                    void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
                    int64_t *col_ind_dev, int32_t *status_dev, mvm_stream_t stream);
+/*
+ * mvm_lsap_solve with host-known bounds on max(rows, cols) over the non-empty
+ * problems (long_max < 1: every problem is empty): kernel classes that cannot
+ * have work are not launched, which matters for small batches of small
+ * problems.  The bounds must hold; mvm_lsap_solve passes (1, INT64_MAX).
+ */
+int mvm_lsap_solve_bounded(const float *cost_dev, const int64_t *cost_offs_dev,
+                           const int64_t *dims_dev, int32_t n_problems,
+                           const int64_t *ws_offs_dev, const int64_t *out_offs_dev,
+                           void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
+                           int64_t *col_ind_dev, int32_t *status_dev, int64_t long_min,
+                           int64_t long_max, mvm_stream_t stream);
 
 /*
  * On-device detection packing, replacing the per-box loop of

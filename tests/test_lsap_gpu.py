@@ -96,3 +96,23 @@ def test_full_256_cube_equals_scipy(cuda, monkeypatch, multi_g):
     r0, c0 = scipy_lsa(flat)
     r1, c1 = linear_sum_assignment(flat)
     assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
+
+
+@pytest.mark.parametrize("shapes", [
+    [(0, 4), (3, 0), (100, 3), (3, 100)],        # no problem in the first wave class, empties
+    [(0, 0), (4, 0)],                             # all empty
+    [(5, 7), (0, 2), (64, 2)],                    # small only
+    [(0, 3), (2000, 5), (1100, 40)],              # workgroup classes + empties
+])
+def test_bounded_launch_sets_every_status(cuda, shapes, lsap_path):
+    """The plan's long-side bounds skip kernel classes without work; every
+    problem (empty ones included) still gets its status and assignment."""
+    rng = np.random.default_rng(3)
+    mats = [rng.normal(size=s).astype(np.float32) for s in shapes]
+    for m, (r, c, st) in zip(mats, _batched(cuda, mats)):
+        assert st == 0
+        if m.size:
+            r0, c0 = scipy_lsa(m)
+            assert np.array_equal(r, r0) and np.array_equal(c, c0)
+        else:
+            assert r.size == 0 and c.size == 0
