@@ -312,6 +312,12 @@ def main():
     avg_dur = float(durs.mean())
     achieved_gbs = float(byts.sum() / durs.sum() / 1e9)
 
+    # ---- the gathered association holds rank 0's rows first (N > 1) -------
+    gather_check = None
+    if env.initialised and env.is_root and gathered is not None:
+        g_am = gathered[0].reshape(-1)[:n_rows].to(argmin.device)
+        gather_check = "rank-0 rows equal after gather" if torch.equal(g_am, argmin) else "MISMATCH"
+
     # ---- parity spot-check of the last launch (untimed) --------------------
     parity = "skipped"
     if env.is_root and wl["mode"] == "pairwise":
@@ -415,7 +421,7 @@ def main():
             "units_per_gpu_step": units_local,
             "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
                             f"({env.backend}{', overlapped per launch' if overlap else ''})")
-                           if world > 1 else "single GPU",
+                           if env.initialised else "single GPU",
         },
         "roofline": {
             "bound": "hbm",
@@ -436,6 +442,8 @@ def main():
         "pcie_inclusive": pcie,
         "parity": parity,
     }
+    if gather_check:
+        out["gather_check"] = gather_check
     if traffic:
         out["roofline"]["traffic_source"] = traffic.get("source")
     print(json.dumps(out), flush=True)

@@ -59,7 +59,10 @@ def init_from_env(backend: Optional[str] = None, use_gpu: bool = True) -> DistEn
     else:
         device = torch.device("cpu")
     initialised = False
-    if world > 1:
+    # MVM_DIST_FORCE=1 creates the process group even for one rank, so the
+    # RCCL code path (device-bound group, async gathers) runs on a 1-GPU box
+    if world > 1 or os.environ.get("MVM_DIST_FORCE") == "1":
+        os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": device} if (use_gpu and backend == "nccl") else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
@@ -124,6 +127,7 @@ class ChunkedRowGather:
         self.env, self.tensors, self.pieces = env, list(tensors), list(pieces)
         self.handles = []
         self.recv = None
+        self.copy_back = []    # (host staging, device destination) of gloo gathers
         if not env.initialised:
             return
         n = torch.tensor([self.tensors[0].numel()], dtype=torch.int64,
@@ -147,8 +151,10 @@ class ChunkedRowGather:
             dst = None
             if self.env.is_root:
                 dst = [self.recv[i][r, a:b] for r in range(self.env.world)]
-                if self.env.backend == "gloo":
-                    dst = [d.cpu() for d in dst]
+                if self.env.backend == "gloo" and dst[0].device.type != "cpu":
+                    host = [torch.empty(d.shape, dtype=d.dtype) for d in dst]
+                    self.copy_back.extend(zip(host, dst))
+                    dst = host
             self.handles.append(dist.gather(src.contiguous(), gather_list=dst, dst=0,
                                             async_op=True))
 
@@ -156,4 +162,7 @@ class ChunkedRowGather:
         for h in self.handles:
             h.wait()
         self.handles = []
+        for host, dev in self.copy_back:
+            dev.copy_(host)
+        self.copy_back = []
         return self.recv

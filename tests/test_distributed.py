@@ -86,3 +86,26 @@ def test_chunked_gather_pieces(tmp_path):
     for r in range(world):
         assert np.array_equal(a[r], np.arange(103) + 1000 * r)
         assert np.array_equal(m[r], np.arange(103, dtype=np.float32) * 0.5 + r)
+
+
+@pytest.mark.gpu
+def test_bench_rccl_process_group_single_rank(tmp_path):
+    """bench.py with the RCCL ("nccl") process group forced at world 1: the
+    device-bound group, the per-launch async gathers into rank 0's receive
+    buffers and the barriers all run on the real backend; the gathered rows
+    equal the local association and the last launch is bit-exact vs the oracle."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MVM_DIST_FORCE="1", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()))
+    env.pop("MVM_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--scenes", "40",
+                        "--chunk", "20", "--steps", "1", "--warmup", "1", "--cpu-seconds", "0"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["gather_check"] == "rank-0 rows equal after gather"
+    assert line["parity"].startswith("bit-exact")
+    assert "nccl" in line["config"]["parallelism"]
