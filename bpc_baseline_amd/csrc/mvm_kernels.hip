@@ -209,6 +209,7 @@ struct PairArgs {
     int32_t lane_results;       // 1: one RPW-lane store per group; 0: one store per row
     int32_t xcd_remap;          // 1: each XCD takes a contiguous range of the logical grid
     int32_t interleave;         // 1: a matrix's row blocks interleave in units of 4*RPW rows
+    int32_t stagger;            // 1: workgroups start their row groups at different offsets
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -221,16 +222,19 @@ struct ColRegs {
 
 // Row stores of the argmin / min of rows r0..r0+RPW-1: lane r holds row r's
 // result (one store instruction with RPW active lanes instead of RPW stores).
+// With a row rotation r_rot, slot r holds row (r + r_rot) mod RPW.
 template <int RPW>
 __device__ __forceinline__ void store_row_results(const uint32_t (&kmin)[RPW],
                                                   const int32_t (&imin)[RPW], int nrows, int lane,
-                                                  int32_t *argmin, float *minval, int64_t row0) {
+                                                  int r_rot, int32_t *argmin, float *minval,
+                                                  int64_t row0) {
     uint32_t k = kKeyInvalid;
     int32_t ix = 0;
+    const int slot = (lane - r_rot) & (RPW - 1);
 #pragma unroll
     for (int r = 0; r < RPW; ++r) {
-        k = (lane == r) ? kmin[r] : k;
-        ix = (lane == r) ? imin[r] : ix;
+        k = (slot == r) ? kmin[r] : k;
+        ix = (slot == r) ? imin[r] : ix;
     }
     if (lane < nrows) {
         if (argmin) argmin[row0 + lane] = (k == kKeyInvalid) ? -1 : ix;
@@ -416,11 +420,20 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     const int n_groups = ilv ? min(args.rows_per_wg / U,
                                    (na - row0 + args.row_blocks * U - 1) / (args.row_blocks * U))
                              : (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
-    for (int g = 0; g < n_groups; ++g) {
+    // with `stagger`, concurrently running workgroups sit at different row
+    // offsets of their blocks (their stores are not 1 MiB-strided in lockstep)
+    const int g_rot = (args.stagger && n_groups > 0) ? (int)(blk % (uint32_t)n_groups) : 0;
+    for (int g_it = 0; g_it < n_groups; ++g_it) {
+        const int g = (g_it + g_rot < n_groups) ? g_it + g_rot : g_it + g_rot - n_groups;
         const int xw = (g * kWaves + wave) * RPW;             // this wave's first local row
         const int grow0 = grow_of(xw);                        // ... and matrix row
         const int nrows = min(RPW, na - grow0);               // scalar, may be <= 0
+        // stagger >= 2 also rotates the row order inside full groups: slot r
+        // holds row (r + r_rot) mod RPW of the group
+        const int r_rot = (args.stagger >= 2 && nrows == RPW)
+                              ? (int)((blk * 5u + (uint32_t)g * 3u) & (uint32_t)(RPW - 1)) : 0;
         if (lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
+            const int slot = (lane - r_rot) & (RPW - 1);
             double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
             bool deg = true;
             if (lane < nrows) {
@@ -428,12 +441,12 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 y = s_rpt[2 * (xw + lane) + 1];
                 deg = row_line(f, x, y, l0, l1, l2);
             }
-            s_row[wave][lane][0] = l0;
-            s_row[wave][lane][1] = l1;
-            s_row[wave][lane][2] = l2;
-            s_row[wave][lane][3] = x;
-            s_row[wave][lane][4] = y;
-            s_row[wave][lane][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
+            s_row[wave][slot][0] = l0;
+            s_row[wave][slot][1] = l1;
+            s_row[wave][slot][2] = l2;
+            s_row[wave][slot][3] = x;
+            s_row[wave][slot][4] = y;
+            s_row[wave][slot][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
         }
         // the same wave reads them back (LDS executes one wave's ops in order)
         const bool rows_fast =
@@ -468,8 +481,10 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 const int jbase = tile * T + c0 + kColsPerLane * lane;
                 const bool fast = rows_fast && __all(clean);   // wave-uniform
                 if (fast && vec_ok) {   // the common case: clean rows, aligned output
-                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    const uint64_t rbase = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+                    uint64_t rp = rbase + (uint64_t)r_rot * rstep;
+                    const uint64_t rwrap = rbase + (uint64_t)RPW * rstep;
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         row_fast<ARGMIN, true, OutT, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
@@ -477,6 +492,7 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                                                s_row[wave][r][4], reinterpret_cast<OutT *>(rp),
                                                jbase, best[r]);
                         rp += rstep;
+                        rp = (rp == rwrap) ? rbase : rp;
                         // keep the row address a running scalar: stops LICM
                         // hoisting all RPW row bases out of the chunk loop
                         // (they would be spilled to VGPR lanes)
@@ -492,7 +508,8 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         if (r < nrows) {
-                            OutT *drow = dbase ? dbase + (int64_t)(grow0 + r) * ld : nullptr;
+                            const int rr = (r + r_rot) & (RPW - 1);
+                            OutT *drow = dbase ? dbase + (int64_t)(grow0 + rr) * ld : nullptr;
                             const bool rdeg = __builtin_amdgcn_readfirstlane(
                                                   (int)s_row[wave][r][5]) == (int)kDeg;
                             row_safe<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
@@ -514,11 +531,11 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 if (r < nrows) wave_argmin(best_key(best[r]), best[r].j, kmin[r], imin[r]);
             }
             if (args.lane_results) {
-                store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                store_row_results<RPW>(kmin, imin, nrows, lane, r_rot, args.argmin, args.minval,
                                        args.row_offs[sp] + grow0);
             } else if (lane == 0) {
                 for (int r = 0; r < nrows; ++r) {
-                    const int64_t row = args.row_offs[sp] + grow0 + r;
+                    const int64_t row = args.row_offs[sp] + grow0 + ((r + r_rot) & (RPW - 1));
                     if (args.argmin) args.argmin[row] = (kmin[r] == kKeyInvalid) ? -1 : imin[r];
                     if (args.minval) args.minval[row] = value_of_key(kmin[r]);
                 }
@@ -808,7 +825,7 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
             imin[r] = 0;
             if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
         }
-        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
                                     roff + (int64_t)i * M + j0);
     }
 }
@@ -1032,7 +1049,7 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
             imin[r] = 0;
             if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
         }
-        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
                                     roff + (int64_t)i * M + j0);
     }
 }
@@ -1272,6 +1289,46 @@ __global__ __launch_bounds__(kThreads) void write_probe_rows_kernel(f32x4 *dst, 
     }
 }
 
+// store-shape model of a residual kernel: workgroups own `rpw * rg` (OWN 1)
+// or `4 * rpw * rg` (OWN 0) rows of 4 KiB, XCD-sequential; OWN 0: wave w owns
+// rpw rows of each group and walks chunk-outer / row-inner (the pairwise
+// kernel, rpw rows open per wave); OWN 1: wave w owns 1-KiB chunk w of every
+// row of the group (the workgroup's 4 waves share rpw open rows)
+// `pace` s_sleep(1) (~64 clocks) after each store stands in for the residual
+// arithmetic between a real kernel's stores
+template <int OWN>
+__global__ __launch_bounds__(kThreads) void write_probe_shape_kernel(f32x4 *dst, size_t n16,
+                                                                     int rpw, int rg, int pace,
+                                                                     float val) {
+    const f32x4 v = {val, val, val, val};
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    uint32_t blk = blockIdx.x;
+    {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const int rows_wg = (OWN == 0 ? 4 : 1) * rpw * rg;
+    const size_t base = (size_t)blk * rows_wg * 256;       // 16-byte units, 256 per row
+    for (int g = 0; g < rg; ++g) {
+        if (OWN == 0) {
+            const int r0 = g * 4 * rpw + wave * rpw;
+            for (int c = 0; c < 4; ++c)
+                for (int r = 0; r < rpw; ++r) {
+                    const size_t i = base + (size_t)(r0 + r) * 256 + c * 64 + lane;
+                    if (i < n16) __builtin_nontemporal_store(v, dst + i);
+                    for (int z = 0; z < pace; ++z) __builtin_amdgcn_s_sleep(1);
+                }
+        } else {
+            const int r0 = g * rpw;
+            for (int r = 0; r < rpw; ++r) {
+                const size_t i = base + (size_t)(r0 + r) * 256 + wave * 64 + lane;
+                if (i < n16) __builtin_nontemporal_store(v, dst + i);
+                for (int z = 0; z < pace; ++z) __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+}
+
 // model of a "16-row unit" decomposition: a persistent grid, workgroup k of
 // XCD x walks units k, k+W, ... of that XCD's eighth; per unit it reads a
 // 44 KiB line block (from a 4 MiB L2-resident region) and writes 64 KiB
@@ -1369,6 +1426,7 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.lane_results = env_int("MVM_PAIRWISE_LANE_RESULTS", 1);
     a.xcd_remap = env_int("MVM_PAIRWISE_XCD", 1);   // MI355X C3: 4.63 vs 4.72 ms per launch
     a.interleave = env_int("MVM_PAIRWISE_INTERLEAVE", 0);
+    a.stagger = env_int("MVM_PAIRWISE_STAGGER", 0);
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
@@ -1555,6 +1613,9 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     f32x4 *d = reinterpret_cast<f32x4 *>(dst_dev);
     const unsigned stride_grid = (unsigned)env_int("MVM_PROBE_GRID", 256 * 8);
+    // MVM_PROBE_LDS: unused dynamic LDS per workgroup (modes 12, 17) to cap the
+    // resident workgroups per CU like a real kernel's footprint does
+    const size_t plds = (size_t)env_int("MVM_PROBE_LDS", 0);
     switch (mode) {
         case 1: write_probe_kernel<4, false><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 2: write_probe_kernel<16, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
@@ -1565,18 +1626,28 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
         case 7: write_probe_pol_kernel<2><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 8: write_probe_pol_kernel<3><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 11: write_probe_kernel<4, true, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
-        case 12: write_probe_rows_kernel<false, true><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 12: write_probe_rows_kernel<false, true><<<(unsigned)((n16 + 16383) / 16384), kThreads, plds, s>>>(d, n16, 1.0f); break;
         case 13: write_probe_kernel<4, false, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 14: write_probe_kernel<4, true, true, true><<<(unsigned)blocks, kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 15: write_probe_kernel<8, true, true><<<(unsigned)((n16 + 8 * kThreads - 1) / (8 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
         case 16: write_probe_kernel<16, true, true><<<(unsigned)((n16 + 16 * kThreads - 1) / (16 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
-        case 17: write_probe_kernel<2, true, true><<<(unsigned)((n16 + 2 * kThreads - 1) / (2 * kThreads)), kThreads, 0, s>>>(d, n16, 1.0f); break;
+        case 17: write_probe_kernel<2, true, true><<<(unsigned)((n16 + 2 * kThreads - 1) / (2 * kThreads)), kThreads, plds, s>>>(d, n16, 1.0f); break;
         case 18: {
             // lines region: the last 4 MiB of the buffer (units stop before it)
             const size_t reserve = (4u << 20) / 16;
             if (n16 <= reserve + 4096) return fail(MVM_ERR_INVALID_ARGUMENT, "buffer too small");
             const unsigned grid = (unsigned)env_int("MVM_PROBE_GRID", 8 * 96);
             write_probe_units_kernel<<<grid, kThreads, 0, s>>>(d, n16 - reserve, d + (n16 - reserve));
+            break;
+        }
+        case 20:
+        case 21: {
+            const int rpw = env_int("MVM_PROBE_RPW", 16), rg = env_int("MVM_PROBE_RG", 4);
+            const int pace = env_int("MVM_PROBE_PACE", 0);
+            const size_t rows_wg = (size_t)(mode == 20 ? 4 : 1) * rpw * rg;
+            const unsigned g = (unsigned)((n16 + rows_wg * 256 - 1) / (rows_wg * 256));
+            if (mode == 20) write_probe_shape_kernel<0><<<g, kThreads, plds, s>>>(d, n16, rpw, rg, pace, 1.0f);
+            else write_probe_shape_kernel<1><<<g, kThreads, plds, s>>>(d, n16, rpw, rg, pace, 1.0f);
             break;
         }
         case 9: write_probe_rows_kernel<false><<<(unsigned)((n16 + 16383) / 16384), kThreads, 0, s>>>(d, n16, 1.0f); break;
