@@ -42,7 +42,7 @@ def _worker(rank, world, port, n_scenes, out_dir):
     torch.distributed.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_sharded_gather_equals_single_process(tmp_path, world):
     from bpc_baseline_amd.synth import make_scenes
     from oracle import oracle as O
