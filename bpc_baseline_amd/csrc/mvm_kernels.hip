@@ -210,6 +210,7 @@ struct PairArgs {
     int32_t xcd_remap;          // 1: each XCD takes a contiguous range of the logical grid
     int32_t interleave;         // 1: a matrix's row blocks interleave in units of 4*RPW rows
     int32_t stagger;            // 1: workgroups start their row groups at different offsets
+    int32_t lazy;               // 1: lazy argmin in clean row groups (chunk tracked, column recovered)
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -328,6 +329,69 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
     }
 }
 
+// ---- lazy argmin (clean row groups) ----
+// In a row group whose rows and columns are all clean (finite, non-degenerate,
+// one column tile), a lane keeps per row only the float32 bits of its minimum
+// (non-negative finite floats order like their bits) and the CHUNK it came
+// from: two v_min3_u32 + one compare + one select per 4 pairs instead of a
+// compare and two selects per pair.  The column inside the chunk is recovered
+// once per group (lane r recomputes the 4 values of row r's winning lane and
+// chunk, `lazy_recover`), so the result is exactly np.argmin's: the earliest
+// chunk wins inside a lane (strict '<'), the lowest q inside a chunk, and
+// rows whose minimum sits in several lanes take the tie path.
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t ab = a < b ? a : b;   // -> v_min3_u32
+    return ab < c ? ab : c;
+}
+
+// float32 bits of the 4 stored values of one lane for one row (row_fast's arithmetic)
+__device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double rl1, double rl2,
+                                           double rx, double ry, float v[kColsPerLane]) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
+        v[q] = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
+    }
+}
+
+template <bool STORE, int NT>
+__device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
+                                              double rx, double ry, float *drow, int jbase,
+                                              uint32_t &bbits, int32_t &bchunk, int32_t cidx) {
+    float v[kColsPerLane];
+    pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
+    if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+    const uint32_t m = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                         __float_as_uint(v[2])),
+                                __float_as_uint(v[3]), bbits);
+    bchunk = (m < bbits) ? cidx : bchunk;
+    bbits = m;
+}
+
+// Column (within the tile) of the first of the 4 values of columns jj0..jj0+3
+// against row line/point `rl`/`rx,ry` whose bits equal `k` (4 if none).
+__device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_l1,
+                                            const double *s_l2, const double *s_x,
+                                            const double *s_y, int jj0, double rl0, double rl1,
+                                            double rl2, double rx, double ry, uint32_t k) {
+    ColRegs c;
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        c.l0[q] = s_l0[jj0 + q];
+        c.l1[q] = s_l1[jj0 + q];
+        c.l2[q] = s_l2[jj0 + q];
+        c.x[q] = s_x[jj0 + q];
+        c.y[q] = s_y[jj0 + q];
+    }
+    float v[kColsPerLane];
+    pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
+    int q = kColsPerLane;
+#pragma unroll
+    for (int p = kColsPerLane - 1; p >= 0; --p) q = (__float_as_uint(v[p]) == k) ? p : q;
+    return q;
+}
+
 // Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair).  The
 // normalised lines of (up to col_tile) columns are computed ONCE per
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
@@ -415,7 +479,11 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     }
     const int n_tiles = (nb + T - 1) / T;
     if (n_tiles == 1) load_tile(0);
-    __syncthreads();
+    // lazy argmin needs every column of the (single) tile clean
+    bool my_clean = n_tiles == 1;
+    if (ARGMIN && sizeof(OutT) == 4 && args.lazy && n_tiles == 1)
+        for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] == kOk);
+    const bool tile_clean = __syncthreads_and(my_clean) != 0;
 
     const int n_groups = ilv ? min(args.rows_per_wg / U,
                                    (na - row0 + args.row_blocks * U - 1) / (args.row_blocks * U))
@@ -455,6 +523,99 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
         Best best[RPW];
 #pragma unroll
         for (int r = 0; r < RPW; ++r) best[r] = Best{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+        // uniform: the whole group takes the lazy argmin (clean rows and tile)
+        const bool lazy = ARGMIN && sizeof(OutT) == 4 && args.lazy && args.row_offs &&
+                          tile_clean && rows_fast && (vec_ok || !dbase);
+        if (lazy) {
+            uint32_t bbits[RPW];
+            int32_t bchunk[RPW];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                bbits[r] = 0x7F800000u;
+                bchunk[r] = 0;
+            }
+            for (int c0 = 0, cidx = 0; c0 < nb; c0 += kChunk, ++cidx) {
+                ColRegs c;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = c0 + kColsPerLane * lane + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
+                }
+                const int jbase = c0 + kColsPerLane * lane;
+                if (dbase) {
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    const uint64_t rbase = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+                    uint64_t rp = rbase + (uint64_t)r_rot * rstep;
+                    const uint64_t rwrap = rbase + (uint64_t)RPW * rstep;
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast_lazy<true, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                                s_row[wave][r][2], s_row[wave][r][3],
+                                                s_row[wave][r][4], reinterpret_cast<float *>(rp),
+                                                jbase, bbits[r], bchunk[r], cidx);
+                        rp += rstep;
+                        rp = (rp == rwrap) ? rbase : rp;
+                        __asm__ volatile("" : "+s"(rp));
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast_lazy<false, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                                 s_row[wave][r][2], s_row[wave][r][3],
+                                                 s_row[wave][r][4], nullptr, jbase, bbits[r],
+                                                 bchunk[r], cidx);
+                }
+            }
+            // per row: wave minimum, its lane and chunk; lane r gathers row r's
+            uint32_t my_k = 0;
+            int32_t my_l = 0, my_c = 0;
+            uint32_t ties = 0;   // rows whose minimum sits in several lanes
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const uint32_t k = wave_min_u32(bbits[r]);
+                const uint64_t hit = __ballot(bbits[r] == k);
+                const int wl = (int)__builtin_ctzll(hit);
+                ties |= (__builtin_popcountll(hit) > 1) ? (1u << r) : 0u;
+                const int wc = __builtin_amdgcn_readlane(bchunk[r], wl);
+                my_k = (lane == r) ? k : my_k;
+                my_l = (lane == r) ? wl : my_l;
+                my_c = (lane == r) ? wc : my_c;
+            }
+            int32_t my_j = 0;
+            if (lane < RPW) {   // lane r recovers the column of row slot r
+                const int jj0 = my_c * kChunk + kColsPerLane * my_l;
+                my_j = jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0, s_row[wave][lane][0],
+                                          s_row[wave][lane][1], s_row[wave][lane][2],
+                                          s_row[wave][lane][3], s_row[wave][lane][4], my_k);
+            }
+            if (ties) {
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    if (!(ties & (1u << r))) continue;   // uniform
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)my_k, r);
+                    uint32_t cand = 0x7FFFFFFFu;
+                    if (bbits[r] == k) {   // every lane holding the minimum finds its first column
+                        const int jj0 = bchunk[r] * kChunk + kColsPerLane * lane;
+                        cand = (uint32_t)(jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0,
+                                                             s_row[wave][r][0], s_row[wave][r][1],
+                                                             s_row[wave][r][2], s_row[wave][r][3],
+                                                             s_row[wave][r][4], k));
+                    }
+                    const int32_t jt = (int32_t)wave_min_u32(cand);
+                    my_j = (lane == r) ? jt : my_j;
+                }
+            }
+            if (lane < nrows) {
+                const int64_t row = args.row_offs[sp] + grow0 + ((lane + r_rot) & (RPW - 1));
+                if (args.argmin) args.argmin[row] = my_j;
+                if (args.minval) args.minval[row] = __uint_as_float(my_k);
+            }
+            continue;
+        }
 
         for (int tile = 0; tile < n_tiles; ++tile) {
             if (n_tiles > 1) {   // large views: stream the column lines tile by tile
@@ -1427,6 +1588,7 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.xcd_remap = env_int("MVM_PAIRWISE_XCD", 1);   // MI355X C3: 4.63 vs 4.72 ms per launch
     a.interleave = env_int("MVM_PAIRWISE_INTERLEAVE", 0);
     a.stagger = env_int("MVM_PAIRWISE_STAGGER", 0);
+    a.lazy = env_int("MVM_PAIRWISE_LAZY", 1);
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);

@@ -47,10 +47,18 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
 
 
 # ----------------------------------------------------------- pairwise ----
+@pytest.fixture(params=["lazy", "eager"])
+def argmin_path(request, monkeypatch):
+    """Run a pairwise test through both argmin paths: the lazy one (clean row
+    groups: per-chunk minimum, column recovered per group) and the eager one."""
+    monkeypatch.setenv("MVM_PAIRWISE_LAZY", "1" if request.param == "lazy" else "0")
+    return request.param
+
+
 @pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),
                                           (4, 3, 37, True), (2, 2, 1, False), (3, 6, 130, True),
                                           (1, 3, 2500, False), (3, 2, 1500, True), (1, 8, 300, True)])
-def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged):
+def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged, argmin_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, C, n, seed=100 + S * n, ragged=ragged)
     assert_pairwise_equal(cuda, b.pts, b.cam_offs, b.F, b.pairs, S, C)
@@ -114,7 +122,7 @@ def test_pairwise_edge_cases(cuda):
     assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C)
 
 
-def test_pairwise_ties_and_duplicates(cuda):
+def test_pairwise_ties_and_duplicates(cuda, argmin_path):
     """Duplicate detections give exact ties across lanes and chunks: lowest index wins."""
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(2, 3, 600, seed=3)
@@ -127,7 +135,27 @@ def test_pairwise_ties_and_duplicates(cuda):
     assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3)
 
 
-def test_pairwise_argmin_only(cuda):
+@pytest.mark.parametrize("n", [256, 512, 1024])
+def test_pairwise_row_minimum_ties(cuda, n, argmin_path):
+    """Exact ties AT the row minimum in clean views (the lazy path's case):
+    a row's winning column is duplicated inside its own 4-column lane group
+    (lower and higher q), in the same lane of another chunk, and in another
+    lane -- np.argmin's lowest index must win every time."""
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(2, 3, n, seed=11 + n)
+    pts = b.pts.copy()
+    _, ra, _, _, _ = O.pairwise(pts, b.cam_offs, b.F, b.pairs, 2, 3, want_dist=False)
+    ro = np.concatenate([[0], np.cumsum([n] * 6)])
+    for s_, p_, row in ((0, 0, 0), (0, 2, 5), (1, 1, 17), (1, 0, n - 1)):
+        cam_b = int(b.pairs[p_][1])
+        j0 = int(ra[ro[s_ * 3 + p_] + row])
+        ob = int(b.cam_offs[s_ * 3 + cam_b])
+        for j in {j0 ^ 1, j0 ^ 3, (j0 + 256) % n, (j0 + 4 * 7 + 1) % n, (j0 + 300) % n}:
+            pts[ob + j] = pts[ob + j0]
+    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3)
+
+
+def test_pairwise_argmin_only(cuda, argmin_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(2, 4, 200, seed=9)
     d, a, m = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False)
