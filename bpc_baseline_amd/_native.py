@@ -13,7 +13,8 @@ import os
 import re
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libmvmatch.so")
+# MVM_LIB_PATH: an alternative in-tree build for A/B timing (tools/ only)
+LIB_PATH = os.environ.get("MVM_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libmvmatch.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "mvmatch.h")
 
 MVM_OK = 0

@@ -146,9 +146,35 @@ def _third_fast_ok_np(q0):
     lo = (b & np.uint64(0xFFFFFFFF)).astype(np.uint32)
     hi = (b >> np.uint64(32)).astype(np.uint32)
     low29 = lo & np.uint32(0x1FFFFFFF)
-    near = (low29 - np.uint32((1 << 28) - 3)) <= np.uint32(6)
-    in_range = ((hi >> np.uint32(20)) - np.uint32(1023 - 126)) <= np.uint32(252)
+    with np.errstate(over="ignore"):
+        near = (low29 - np.uint32((1 << 28) - 3)) <= np.uint32(6)
+        in_range = ((hi >> np.uint32(20)) - np.uint32(1023 - 126)) <= np.uint32(252)
     return ~near & in_range
+
+
+def _third_fast_ok_spec(q0):
+    """The rule as first written: |low 29 mantissa bits - 2^28| <= 3 is near a
+    float32 midpoint; the exponent must put q0 in [2^-126, 2^127)."""
+    b = q0.view(np.uint64)
+    lo = (b & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    e = (b >> np.uint64(52)).astype(np.int64)              # sign + exponent
+    near = np.abs((lo & 0x1FFFFFFF) - (1 << 28)) <= 3
+    in_range = (e >= 1023 - 126) & (e <= 1023 + 126)
+    return ~near & in_range
+
+
+def test_third_fast_ok_bit_form_equals_spec():
+    """The kernel's wrap-around form of the check equals the spec on random bit
+    patterns, every low-29 value around 2^28 and the exponent window edges."""
+    rng = np.random.default_rng(1)
+    bits = rng.integers(0, 2 ** 63, 2_000_000, dtype=np.uint64)
+    bits[::2] |= np.uint64(1) << np.uint64(63)                    # negatives too
+    lows = np.arange((1 << 28) - 40, (1 << 28) + 40, dtype=np.uint64)
+    exps = np.array([0, 1, 896, 897, 898, 1149, 1150, 1151, 2046, 2047], dtype=np.uint64)
+    grid = (exps[:, None] << np.uint64(52)) | lows[None, :] | (np.uint64(0x5A5A5) << np.uint64(29))
+    q0 = np.concatenate([bits, grid.reshape(-1), grid.reshape(-1) | (np.uint64(1) << np.uint64(63))])
+    q0 = q0.view(np.float64)
+    assert np.array_equal(_third_fast_ok_np(q0.copy()), _third_fast_ok_spec(q0.copy()))
 
 
 def test_fast_division_by_three_rule():
