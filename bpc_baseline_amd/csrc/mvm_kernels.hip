@@ -1592,7 +1592,16 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
-    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg);
+    // MVM_PAIRWISE_LDS_PAD (experiments): unused LDS per workgroup, to cap the
+    // resident workgroups per CU
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg) +
+                       (size_t)max(0, env_int("MVM_PAIRWISE_LDS_PAD", 0));
+    if (lds > 65536) {
+        const void *fns[] = {reinterpret_cast<const void *>(&pairwise_kernel<RPW, true, float, 1>),
+                             reinterpret_cast<const void *>(&pairwise_kernel<RPW, false, float, 1>)};
+        for (const void *fn : fns)
+            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
     if (f64) {
         pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
     } else {

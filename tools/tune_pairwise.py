@@ -19,7 +19,7 @@ ap.add_argument("--scenes", type=int, default=1000)
 ap.add_argument("--cams", type=int, default=4)
 ap.add_argument("--dets", type=int, default=1024)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="4,8,16", help="RPW or RPW:RG[:LANE_RESULTS[:NT[:XCD[:INTERLEAVE[:STAGGER[:LAZY]]]]]] list")
+ap.add_argument("--variants", default="4,8,16", help="RPW or RPW:RG[:LANE_RESULTS[:NT[:XCD[:INTERLEAVE[:STAGGER[:LAZY[:LDS_PAD]]]]]]] list")
 ap.add_argument("--no-dist", action="store_true")
 ap.add_argument("--no-argmin", action="store_true", help="distances only (argmin template off)")
 args = ap.parse_args()
@@ -46,6 +46,8 @@ for rnd in range(args.rounds + 1):
         xcd, _, ilv = xcd.partition(":")
         ilv, _, stg = ilv.partition(":")
         stg, _, lazy = stg.partition(":")
+        lazy, _, pad = lazy.partition(":")
+        os.environ["MVM_PAIRWISE_LDS_PAD"] = pad or "0"
         os.environ["MVM_PAIRWISE_STAGGER"] = stg or "0"
         os.environ["MVM_PAIRWISE_LAZY"] = lazy or "1"
         os.environ["MVM_PAIRWISE_INTERLEAVE"] = ilv or "0"
