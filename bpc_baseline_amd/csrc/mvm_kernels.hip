@@ -311,12 +311,31 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
     }
 }
 
+// Clean row of a matrix whose rows are not 16-byte aligned (n_b % 4 != 0):
+// the lane holds columns jbase + 64q, so each of the 4 dword stores writes 256
+// contiguous bytes.  Default store policy: a row's first and last lines are
+// shared with its neighbours and L2 merges them (nontemporal partial lines
+// reach HBM as masked writes, ~3.7x slower).
+template <bool ARGMIN>
+__device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, double rl1,
+                                                 double rl2, double rx, double ry, float *drow,
+                                                 int jbase, Best &best) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
+        const float v = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
+        drow[jbase + kWave * q] = v;
+        if (ARGMIN) best_update_fast(best, v, jbase + kWave * q);
+    }
+}
+
 // Generic row: degenerate lines (9999 sentinel), non-finite or huge values,
-// tails, unaligned rows, no output buffer.
+// tails, unaligned rows, no output buffer.  Column of slot q: jbase + q*jstep.
 template <bool ARGMIN, typename OutT>
 __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, bool rdeg, OutT *drow, int jbase,
-                                         int nb, Best &best) {
+                                         int jstep, Best &best) {
 #pragma unroll
     for (int q = 0; q < kColsPerLane; ++q) {
         double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);
@@ -324,8 +343,9 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
         const double d2 = rdeg ? kSentinel : line_dist(rl0, rl1, rl2, c.x[q], c.y[q]);
         const double e = 0.5 * (d1 + d2);                                            // :28
         const bool valid = c.state[q] != kNone;
-        if (drow && valid) __builtin_nontemporal_store((OutT)e, drow + jbase + q);
-        if (ARGMIN && valid) best_update_safe(best, (float)e, jbase + q);
+        const int j = jbase + q * jstep;
+        if (drow && valid) drow[j] = (OutT)e;   // default policy: L2 merges partial lines
+        if (ARGMIN && valid) best_update_safe(best, (float)e, j);
     }
 }
 
@@ -449,6 +469,8 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     const int64_t ld = args.ld ? args.ld : nb;
     OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
     const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
+    // unaligned float32 rows: lanes take strided columns (coalesced dword stores)
+    const bool strided = dbase && !vec_ok && sizeof(OutT) == 4;
 
     // column lines of columns [c0, c0 + T) -> LDS (threads stride the tile)
     auto load_tile = [&](int c0) {
@@ -630,7 +652,7 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 bool clean = true;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-                    const int jj = c0 + kColsPerLane * lane + q;
+                    const int jj = strided ? c0 + lane + kWave * q : c0 + kColsPerLane * lane + q;
                     c.l0[q] = s_l0[jj];
                     c.l1[q] = s_l1[jj];
                     c.l2[q] = s_l2[jj];
@@ -639,9 +661,20 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     c.state[q] = s_cst[jj];
                     clean &= (c.state[q] == kOk);
                 }
-                const int jbase = tile * T + c0 + kColsPerLane * lane;
+                const int jbase = tile * T + c0 + (strided ? lane : kColsPerLane * lane);
+                const int jstep = strided ? kWave : 1;
                 const bool fast = rows_fast && __all(clean);   // wave-uniform
-                if (fast && vec_ok) {   // the common case: clean rows, aligned output
+                if (fast && strided && sizeof(OutT) == 4) {   // clean rows, unaligned output
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        const int rr = (r + r_rot) & (RPW - 1);
+                        row_fast_strided<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
+                                                 s_row[wave][r][2], s_row[wave][r][3],
+                                                 s_row[wave][r][4],
+                                                 reinterpret_cast<float *>(dbase + (int64_t)(grow0 + rr) * ld),
+                                                 jbase, best[r]);
+                    }
+                } else if (fast && vec_ok) {   // the common case: clean rows, aligned output
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
                     const uint64_t rbase = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
                     uint64_t rp = rbase + (uint64_t)r_rot * rstep;
@@ -675,7 +708,7 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                                                   (int)s_row[wave][r][5]) == (int)kDeg;
                             row_safe<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
                                              s_row[wave][r][2], s_row[wave][r][3],
-                                             s_row[wave][r][4], rdeg, drow, jbase, nb, best[r]);
+                                             s_row[wave][r][4], rdeg, drow, jbase, jstep, best[r]);
                         }
                     }
                 }
@@ -780,7 +813,7 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
                 } else {
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q)
-                        if (kbase + q < P) __builtin_nontemporal_store((float)e[q], crow + kbase + q);
+                        if (kbase + q < P) crow[kbase + q] = (float)e[q];   // L2 merges strided dwords
                 }
             }
 #pragma unroll
@@ -900,7 +933,9 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
     const int kvalid = P - kb;
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
-    const bool full = (P == kChunk) && ((coff & 3) == 0) && args.cube;
+    // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
+    const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+    const bool act = kvalid > 0;
 
     // ---- prologue: all loads of the tile, then one barrier ----------------
     double a23[kCubeRPW][kColsPerLane];
@@ -952,25 +987,35 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
             }
             float v[kColsPerLane];
             const int64_t row = (int64_t)i * M + j0 + r;
-            if (full && __all(ok)) {
+            if (full && __all(ok || !act)) {
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                              (uint32_t)kb * 4u, v);
+                if (act) {
+                    store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                  (uint32_t)kb * 4u, v);
+                }
                 Best b{v[0], kb};
 #pragma unroll
                 for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                key[r] = __float_as_uint(b.v) + 1u;
-                idx[r] = b.j;
+                key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                idx[r] = act ? b.j : 0x7FFFFFFF;
             } else {
                 Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                // the IEEE division only when some lane needs it (uniform branch)
+                double qq[kColsPerLane];
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                if (!__all(ok || !act)) {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q)
+                        qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                }
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                    v[q] = (float)qq;
+                    v[q] = (float)qq[q];
                     if (q < kvalid) {
                         if (args.cube)
-                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                            args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
                         best_update_safe(b, v[q], kb + q);
                     }
                 }
@@ -1062,7 +1107,9 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
     const int kvalid = P - kb;
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
-    const bool full = (P == kChunk) && ((coff & 3) == 0) && args.cube;
+    // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
+    const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+    const bool act = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
     const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
@@ -1176,25 +1223,35 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
             }
             float v[kColsPerLane];
             const int64_t row = (int64_t)i * M + j0 + r;
-            if (full && __all(ok)) {
+            if (full && __all(ok || !act)) {
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                              (uint32_t)kb * 4u, v);
+                if (act) {
+                    store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                  (uint32_t)kb * 4u, v);
+                }
                 Best b{v[0], kb};
 #pragma unroll
                 for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                key[r] = __float_as_uint(b.v) + 1u;
-                idx[r] = b.j;
+                key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                idx[r] = act ? b.j : 0x7FFFFFFF;
             } else {
                 Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                // the IEEE division only when some lane needs it (uniform branch)
+                double qq[kColsPerLane];
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                if (!__all(ok || !act)) {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q)
+                        qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                }
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-                    const double qq = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                    v[q] = (float)qq;
+                    v[q] = (float)qq[q];
                     if (q < kvalid) {
                         if (args.cube)
-                            __builtin_nontemporal_store(v[q], args.cube + coff + row * P + kb + q);
+                            args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
                         best_update_safe(b, v[q], kb + q);
                     }
                 }
@@ -1212,6 +1269,241 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
         }
         store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
                                     roff + (int64_t)i * M + j0);
+    }
+}
+
+// ------------------------------------ fused tiled cube, any P (v5) ----
+// triplet_fused_kernel for views of more than 256 detections: the k axis is
+// walked in chunks of 256.  Per chunk the prologue computes that chunk's
+// e13 [IB][256] (LDS) and the wave's e23 [RPW j][4 k] (registers) exactly as
+// the single-chunk kernel does; the tile's view-0 / view-1 lines and e12 are
+// computed once.  Each (i, j) row's argmin runs across chunks in two lane-
+// distributed registers (row x = ii*RPW + r lives in lane x % 64, slot x / 64):
+// a chunk's wave minimum replaces the running one only if strictly smaller,
+// so the earliest chunk wins ties (np.argmin's first index).
+template <int kCubeIB, int kCubeRPW>
+__global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFusedArgs args) {
+    constexpr int kJ = kWaves * kCubeRPW;
+    constexpr int kRows = kCubeIB * kCubeRPW;                                      // (i, j) rows per wave
+    constexpr int kSlots = (kRows + kWave - 1) / kWave;
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
+    __shared__ LineRec s_r13[kCubeIB], s_r12[kCubeIB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[kCubeIB][2], s_p1[kJ][2];
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    uint32_t blk = blockIdx.x;
+    if (args.xcd_remap) {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blk / per_scene);
+    const int rem = (int)(blk % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
+    const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
+    const int jw0 = jb * kJ;
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;
+    const int nrows = min(kCubeRPW, M - j0);
+    const int kb = kColsPerLane * lane;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
+    const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
+    const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
+
+    // ---- once per tile: view-0 rows, view-1 rows/columns, e12 ---------------
+    if (t < kCubeIB) {
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (t < ni) {
+            double f[9];
+            px = args.pts[2 * (c0 + i0 + t)];
+            py = args.pts[2 * (c0 + i0 + t) + 1];
+            load_f(F13, f);
+            a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F12, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_r13[t] = a;
+        s_r12[t] = b;
+        s_p0[t][0] = px;
+        s_p0[t][1] = py;
+    } else if (t >= kWave && t < kWave + kJ) {
+        const int jj = t - kWave;
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (jw0 + jj < M) {
+            double f[9];
+            px = args.pts[2 * (c1 + jw0 + jj)];
+            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            load_f(F12, f);
+            a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_c12[jj] = a;
+        s_r23[jj] = b;
+        s_p1[jj][0] = px;
+        s_p1[jj][1] = py;
+    }
+    __syncthreads();
+    for (int x = t; x < kCubeIB * kJ; x += kThreads) {
+        const int r = x / kJ, jj = x % kJ;
+        s12[r][jj] = (r < ni && jw0 + jj < M)
+                         ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                         : 0.0;
+    }
+    uint32_t run_k[kSlots];
+    int32_t run_i[kSlots];
+#pragma unroll
+    for (int z = 0; z < kSlots; ++z) {
+        run_k[z] = kKeyInvalid;
+        run_i[z] = 0;
+    }
+
+    for (int kc = 0; kc < P; kc += kChunk) {
+        const int Pc = min(kChunk, P - kc);
+        const int kvalid = Pc - kb;
+        if (kc > 0) __syncthreads();   // every wave is done with the previous chunk's s13
+        {   // e13 of this chunk: one column per thread
+            const int k = t;
+            double f13[9];
+            load_f(F13, f13);
+            if (k < Pc) {
+                const double x = args.pts[2 * (c2 + kc + k)], y = args.pts[2 * (c2 + kc + k) + 1];
+                LineRec cl{0.0, 0.0, 0.0, 0.0};
+                cl.deg = col_line(f13, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+#pragma unroll 4
+                for (int r = 0; r < kCubeIB; ++r)
+                    s13[r][k] = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+            } else {
+                for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
+            }
+        }
+        double a23[kCubeRPW][kColsPerLane];
+        double f23[9];
+        load_f(F23, f23);
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) {
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            double x = 0.0, y = 0.0;
+            if (q < kvalid) {
+                x = args.pts[2 * (c2 + kc + kb + q)];
+                y = args.pts[2 * (c2 + kc + kb + q) + 1];
+                cl.deg = col_line(f23, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                const int jj = wave * kCubeRPW + r;
+                a23[r][q] = (r < nrows && q < kvalid)
+                                ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
+                                : 0.0;
+            }
+        }
+        __syncthreads();
+        if (nrows <= 0) continue;   // uniform; the barriers above are still reached
+
+        const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+        const bool act = kvalid > 0;
+        for (int ii = 0; ii < ni; ++ii) {
+            const int i = i0 + ii;
+            double a13[kColsPerLane];
+            {
+                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+            }
+            uint32_t key[kCubeRPW];
+            int32_t idx[kCubeRPW];
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                key[r] = kKeyInvalid;
+                idx[r] = 0x7FFFFFFF;
+                if (r >= nrows) continue;   // uniform
+                const double v12 = s12[ii][wave * kCubeRPW + r];
+                double sum[kColsPerLane], q0[kColsPerLane];
+                bool ok = true;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                    q0[q] = sum[q] * kThird;
+                    ok &= third_fast_ok(q0[q]);
+                }
+                float v[kColsPerLane];
+                const int64_t row = (int64_t)i * M + j0 + r;
+                if (full && __all(ok || !act)) {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                    if (act) {
+                        store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
+                                      (uint32_t)kb * 4u, v);
+                    }
+                    Best b{v[0], kb};
+#pragma unroll
+                    for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                    key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                    idx[r] = act ? b.j : 0x7FFFFFFF;
+                } else {
+                    Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                    // the IEEE division only when some lane needs it (uniform branch)
+                    double qq[kColsPerLane];
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                    if (!__all(ok || !act)) {
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q)
+                            qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) {
+                        v[q] = (float)qq[q];
+                        if (q < kvalid) {
+                            if (args.cube)
+                                args.cube[coff + row * P + kc + kb + q] = v[q];
+                            best_update_safe(b, v[q], kb + q);
+                        }
+                    }
+                    key[r] = best_key(b);
+                    idx[r] = b.j;
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                if (r >= nrows) continue;
+                uint32_t km;
+                int32_t im;
+                wave_argmin(key[r], idx[r], km, im);
+                const int x = ii * kCubeRPW + r;   // uniform
+                const bool mine = lane == (x % kWave);
+#pragma unroll
+                for (int z = 0; z < kSlots; ++z) {
+                    if (z != x / kWave) continue;   // uniform
+                    const bool take = mine && km < run_k[z];
+                    run_k[z] = take ? km : run_k[z];
+                    run_i[z] = take ? kc + im : run_i[z];
+                }
+            }
+        }
+    }
+    if (nrows <= 0) return;
+#pragma unroll
+    for (int z = 0; z < kSlots; ++z) {
+        const int x = z * kWave + lane;
+        const int ii = x / kCubeRPW, r = x % kCubeRPW;
+        if (x < kRows && ii < ni && r < nrows) {
+            const int64_t row = roff + (int64_t)(i0 + ii) * M + j0 + r;
+            if (args.argmin) args.argmin[row] = (run_k[z] == kKeyInvalid) ? -1 : run_i[z];
+            if (args.minval) args.minval[row] = value_of_key(run_k[z]);
+        }
     }
 }
 
@@ -1912,6 +2204,27 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
         default: triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c); break;
         }
         return check_launch("triplet_fused_kernel");
+    }
+    if (max_n > kChunk && variant == 3 && env_int("MVM_TRIPLET_CHUNKED", 1)) {
+        // views of more than 256: fused tiles walking k in chunks of 256
+        CubeFusedArgs c{};
+        c.pts = pts_dev;
+        c.cam_offs = cam_offs_dev;
+        c.F = F_dev;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.xcd_remap = env_int("MVM_TRIPLET_XCD", 0);
+        c.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+        c.i_blocks = (max_n + 16 - 1) / 16;
+        const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
+        if (blocks > 0x7FFFFFFFLL)
+            return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+        triplet_fused_chunked_kernel<16, 8><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+        return check_launch("triplet_fused_chunked_kernel");
     }
     const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;
     const int64_t mat_stride = (int64_t)max_n * ld;

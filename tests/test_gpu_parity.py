@@ -169,9 +169,11 @@ def test_pairwise_argmin_only(cuda, argmin_path):
 def cube_path(request, monkeypatch):
     """Run a cube test through each cube kernel: the small-scene kernel (views
     of <= 64 detections), the fused tiled kernel (pair residuals computed in
-    the prologue; default up to 256) and the tiled kernel + fp64 workspace."""
+    the prologue; default up to 256, then its k-chunked form) and the tiled
+    kernel + fp64 workspace (beyond 256: the generic kernel)."""
     monkeypatch.setenv("MVM_TRIPLET_SMALL", "1" if request.param == "small" else "0")
     monkeypatch.setenv("MVM_TRIPLET_FUSED", "0" if request.param == "tiled" else "1")
+    monkeypatch.setenv("MVM_TRIPLET_CHUNKED", "0" if request.param == "tiled" else "1")
     return request.param
 
 
@@ -201,7 +203,9 @@ def test_cube_golden_batched(cuda, golden, cube_path):
 
 
 @pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False),
-                                        (300, 24, False), (40, 64, True), (7, 1, False)])
+                                        (300, 24, False), (40, 64, True), (7, 1, False),
+                                        (2, 512, False), (3, 333, True), (1, 770, False), (2, 200, False),
+                                        (2, 384, False)])
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
@@ -262,3 +266,24 @@ def test_launches_capture_into_a_hip_graph(cuda):
     for x, r in zip((dist, am, cube, cam), ref):
         assert torch.equal(x.view(torch.int32) if x.dtype == torch.float32 else x,
                            r.view(torch.int32) if r.dtype == torch.float32 else r)
+
+
+def test_cube_row_minimum_ties_across_chunks(cuda, cube_path):
+    """Views of more than 256: a row's winning k duplicated in its own lane
+    group, in the same lane of the next 256-chunk and in the ragged tail chunk;
+    the lowest k must win (the chunked kernel keeps the earliest chunk)."""
+    from bpc_baseline_amd.synth import make_scenes
+    n = 520
+    b = make_scenes(1, 3, n, seed=21)
+    pts = b.pts.copy()
+    _, ra, _, _, _ = O.cube(pts, b.cam_offs, b.F, 1, want_cube=False)
+    o3 = int(b.cam_offs[2])
+    for row in (0, 77):
+        k0 = int(ra[row])
+        for k in {k0 ^ 1, (k0 + 256) % n, (k0 + 260) % n, n - 3}:
+            pts[o3 + k] = pts[o3 + k0]
+    c, a, m = run_cube(cuda, pts, b.cam_offs, b.F, 1)
+    rc, ra, rm, _, _ = O.cube(pts, b.cam_offs, b.F, 1)
+    assert np.array_equal(_bits(c), _bits(rc))
+    assert np.array_equal(a, ra)
+    assert np.array_equal(_bits(m), _bits(rm))
