@@ -284,7 +284,9 @@ __device__ __forceinline__ uint32_t best_key(const Best &b) {
 
 // One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
 // per pair, one 16-byte store, 3 int ops of argmin per pair.
-template <bool ARGMIN, bool STORE, typename OutT, int NT = 1>
+// MASK: the tail chunk of an aligned matrix (n_b % 4 == 0): a lane's 4 columns
+// are all in the view or all past it (state kNone), and only the former store.
+template <bool ARGMIN, bool STORE, typename OutT, int NT = 1, bool MASK = false>
 __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, OutT *drow, int jbase, Best &best) {
     double e[kColsPerLane];
@@ -301,6 +303,7 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
         }
     }
     if constexpr (sizeof(OutT) == 4) {
+        if (MASK && c.state[0] == kNone) return;
         if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
         if (ARGMIN) {
 #pragma unroll
@@ -316,6 +319,8 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
 // contiguous bytes.  Default store policy: a row's first and last lines are
 // shared with its neighbours and L2 merges them (nontemporal partial lines
 // reach HBM as masked writes, ~3.7x slower).
+// Also the tail chunk of any float32 matrix: columns past the view (kNone) are
+// skipped per lane.  drow == nullptr: association only.
 template <bool ARGMIN>
 __device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, double rl1,
                                                  double rl2, double rx, double ry, float *drow,
@@ -325,8 +330,10 @@ __device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, d
         const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
         const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
         const float v = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
-        drow[jbase + kWave * q] = v;
-        if (ARGMIN) best_update_fast(best, v, jbase + kWave * q);
+        if (c.state[q] != kNone) {
+            if (drow) drow[jbase + kWave * q] = v;
+            if (ARGMIN) best_update_fast(best, v, jbase + kWave * q);
+        }
     }
 }
 
@@ -648,11 +655,15 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
             const int tile_cols = min(T, nb - tile * T);
             if (nrows <= 0) continue;
             for (int c0 = 0; c0 < tile_cols; c0 += kChunk) {
+                // strided columns for unaligned rows; an aligned matrix's tail chunk
+                // keeps 16-byte stores, masked per lane
+                const bool str = strided;
+                const bool tail = sizeof(OutT) == 4 && c0 + kChunk > tile_cols;
                 ColRegs c;
-                bool clean = true;
+                bool clean = true, clean_m = true;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-                    const int jj = strided ? c0 + lane + kWave * q : c0 + kColsPerLane * lane + q;
+                    const int jj = str ? c0 + lane + kWave * q : c0 + kColsPerLane * lane + q;
                     c.l0[q] = s_l0[jj];
                     c.l1[q] = s_l1[jj];
                     c.l2[q] = s_l2[jj];
@@ -660,19 +671,32 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     c.y[q] = s_y[jj];
                     c.state[q] = s_cst[jj];
                     clean &= (c.state[q] == kOk);
+                    clean_m &= (c.state[q] == kOk || c.state[q] == kNone);
                 }
-                const int jbase = tile * T + c0 + (strided ? lane : kColsPerLane * lane);
-                const int jstep = strided ? kWave : 1;
+                const int jbase = tile * T + c0 + (str ? lane : kColsPerLane * lane);
+                const int jstep = str ? kWave : 1;
                 const bool fast = rows_fast && __all(clean);   // wave-uniform
-                if (fast && strided && sizeof(OutT) == 4) {   // clean rows, unaligned output
+                if (str && rows_fast && __all(clean_m)) {   // clean rows: unaligned output or tail
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         const int rr = (r + r_rot) & (RPW - 1);
                         row_fast_strided<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
                                                  s_row[wave][r][2], s_row[wave][r][3],
                                                  s_row[wave][r][4],
-                                                 reinterpret_cast<float *>(dbase + (int64_t)(grow0 + rr) * ld),
+                                                 dbase ? reinterpret_cast<float *>(dbase + (int64_t)(grow0 + rr) * ld)
+                                                       : nullptr,
                                                  jbase, best[r]);
+                    }
+                } else if (tail && vec_ok && rows_fast && __all(clean_m)) {   // aligned tail chunk
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    const uint64_t rbase = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        const int rr = (r + r_rot) & (RPW - 1);
+                        row_fast<ARGMIN, true, OutT, NT, true>(
+                            c, s_row[wave][r][0], s_row[wave][r][1], s_row[wave][r][2],
+                            s_row[wave][r][3], s_row[wave][r][4],
+                            reinterpret_cast<OutT *>(rbase + (uint64_t)rr * rstep), jbase, best[r]);
                     }
                 } else if (fast && vec_ok) {   // the common case: clean rows, aligned output
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
@@ -1897,7 +1921,9 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     if (f64) {
         pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
     } else {
-        switch (env_int("MVM_PAIRWISE_NT", 1)) {
+        // nontemporal stores for whole-line rows; rows that end mid-line share
+        // that line with the next row, and L2 must merge it (default policy)
+        switch (env_int("MVM_PAIRWISE_NT", (max_cols % 32 == 0) ? 1 : 0)) {
         case 0:
             if (argmin) pairwise_kernel<RPW, true, float, 0><<<grid, block, lds, stream>>>(a);
             else pairwise_kernel<RPW, false, float, 0><<<grid, block, lds, stream>>>(a);
