@@ -33,13 +33,41 @@ import torch
 from .. import ops
 from .utils.camera_utils import camera_pairs, fundamental_matrices_batched
 
-__all__ = ["MatchBatch", "match_captures", "projection_matrices"]
+__all__ = ["MatchBatch", "match_captures", "projection_matrices", "rig_matrices"]
 
 
 def projection_matrices(Ks: np.ndarray, RTs: np.ndarray) -> np.ndarray:
     """P = K @ RT[:3] per camera (process_pose.py:91: float32 K promoted to
     float64 by the product with the float64 RT) -> float64 [S, C, 3, 4]."""
     return np.ascontiguousarray(np.asarray(Ks) @ np.asarray(RTs, dtype=np.float64)[..., :3, :])
+
+
+def rig_matrices(Ks: np.ndarray, RTs: np.ndarray):
+    """F (f64 [S*3, 9]) and P (f64 [S, 3, 3, 4]) of every capture, computed once
+    per DISTINCT rig: captures whose K and RT bytes are identical (a static
+    camera rig, as within an IPD scene) share one evaluation, so the values
+    are bit-identical to evaluating each capture."""
+    S = Ks.shape[0]
+    kb = np.ascontiguousarray(Ks).reshape(S, -1).view(np.uint32)
+    rb = np.ascontiguousarray(RTs).reshape(S, -1).view(np.uint64)
+    if S > 1 and (kb == kb[0]).all() and (rb == rb[0]).all():
+        first, inv = np.zeros(1, np.int64), np.zeros(S, np.int64)
+    elif S > 1 and len(np.unique(rb[:, 3])) == S:   # camera 0's t_x already tells them apart
+        first, inv = None, None
+    elif S > 1:
+        key = np.ascontiguousarray(np.concatenate([kb.view(np.uint8), rb.view(np.uint8)], axis=1))
+        kv = key.view(np.dtype((np.void, key.shape[1]))).reshape(-1)
+        _, first, inv = np.unique(kv, return_index=True, return_inverse=True)
+        inv = inv.reshape(-1)
+        if len(first) == S:
+            first, inv = None, None
+    else:
+        first, inv = None, None
+    if first is None:
+        return fundamental_matrices_batched(Ks, RTs, camera_pairs(3)), projection_matrices(Ks, RTs)
+    Fu = fundamental_matrices_batched(Ks[first], RTs[first], camera_pairs(3)).reshape(len(first), 3, 9)
+    Pu = projection_matrices(Ks[first], RTs[first])
+    return np.ascontiguousarray(Fu[inv].reshape(S * 3, 9)), np.ascontiguousarray(Pu[inv])
 
 
 @dataclass
@@ -111,11 +139,16 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     pts, cam_offs, boxes_int, counts, status = ops.pack_detections(boxes, conf, cls, img_offs,
                                                                    conf_thresh)
     mark("pack")
-    # host work while the packing runs: F and P for every capture
-    if F is None:
-        F = torch.from_numpy(fundamental_matrices_batched(Ks, RTs, camera_pairs(3))).to(dev)
+    # host work while the packing runs: F and P for every capture (once per
+    # distinct rig)
+    if F is None or proj is None:
+        F_h, P_h = rig_matrices(Ks, RTs)
+        if F is None:
+            F = torch.from_numpy(F_h).to(dev)
+        if proj is None:
+            proj = torch.from_numpy(P_h).to(dev)
     F_dev = F.reshape(-1)
-    proj_dev = torch.from_numpy(projection_matrices(Ks, RTs)).to(dev) if proj is None else proj
+    proj_dev = proj
     mark("F+P host")
 
     # one device -> host copy: the kept counts and the packing status

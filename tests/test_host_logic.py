@@ -274,3 +274,22 @@ def test_reference_loop_restatement_is_bit_exact(golden):
         F12, F13, F23 = (np.asarray(f, np.float64).reshape(3, 3) for f in g[f"{n}_F"])
         c = RL.cube(g[f"{n}_p1"], g[f"{n}_p2"], g[f"{n}_p3"], F12, F13, F23)
         assert np.array_equal(c.view(np.int32), g[f"{n}_cube"].view(np.int32)), n
+
+
+@pytest.mark.parametrize("mode", ["static", "mixed", "distinct", "single"])
+def test_rig_matrices_dedupe_bit_equal(mode):
+    """match_captures' F/P: one evaluation per distinct rig, bit-equal to
+    evaluating every capture (static rig, a few rigs, all distinct, S = 1)."""
+    from bpc_baseline_amd.synth import make_rig
+    from bpc_baseline_amd.inference.batch_match import projection_matrices, rig_matrices
+    from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs, fundamental_matrices_batched
+    rng = np.random.default_rng(4)
+    S = 1 if mode == "single" else 64
+    rigs = [make_rig(rng, 3) for _ in range(S if mode == "distinct" else 3)]
+    idx = {"static": np.zeros(S, int), "mixed": rng.integers(0, 3, S),
+           "distinct": np.arange(S), "single": np.zeros(S, int)}[mode]
+    Ks = np.stack([np.stack(rigs[i][0]) for i in idx]).astype(np.float32)
+    RTs = np.stack([np.stack(rigs[i][1]) for i in idx]).astype(np.float64)
+    F, P = rig_matrices(Ks, RTs)
+    assert np.array_equal(F.view(np.int64), fundamental_matrices_batched(Ks, RTs, camera_pairs(3)).view(np.int64))
+    assert np.array_equal(P.view(np.int64), projection_matrices(Ks, RTs).view(np.int64))

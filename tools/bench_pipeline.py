@@ -47,9 +47,14 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=50)
+    ap.add_argument("--rig-group", type=int, default=1,
+                    help="consecutive captures sharing one camera rig (IPD: the images of a scene)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     b = make_detector_batch(args.captures, args.dets, seed=5)
+    if args.rig_group > 1:   # rig of the group's first capture (match_captures dedupes F/P)
+        src = np.arange(args.captures) // args.rig_group * args.rig_group
+        b.Ks, b.RTs = np.ascontiguousarray(b.Ks[src]), np.ascontiguousarray(b.RTs[src])
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     boxes, conf, cls, offs = t(b.boxes), t(b.conf), t(b.cls), t(b.img_offs)
     res = None
@@ -95,7 +100,8 @@ def main():
     print(json.dumps({
         "metric": "captures matched/sec (detect-pack + cube + LSAP + select + DLT)",
         "value": args.captures / dt, "unit": "captures/s", "ms_per_batch": dt * 1e3,
-        "config": {"captures": args.captures, "dets_per_view": args.dets, "cams": 3},
+        "config": {"captures": args.captures, "dets_per_view": args.dets, "cams": 3,
+                   "captures_per_rig": args.rig_group},
         "matches": int(res.count.sum()), "parity_checked": len(check),
         "stage_ms_synchronised": stages,
         "static_rig": {"value": args.captures / dt_cached, "ms_per_batch": dt_cached * 1e3,
