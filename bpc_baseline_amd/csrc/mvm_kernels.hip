@@ -425,7 +425,7 @@ __device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
 template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
-__global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
+__global__ __launch_bounds__(kThreads, 3) void pairwise_kernel(PairArgs args) {   // 3 waves/SIMD: <= 168 VGPRs
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
     double *s_l0 = reinterpret_cast<double *>(s_dyn);
@@ -433,8 +433,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     double *s_l2 = s_l1 + T;
     double *s_x = s_l2 + T;
     double *s_y = s_x + T;
-    double(*s_row)[RPW][6] = reinterpret_cast<double(*)[RPW][6]>(s_y + T);   // per wave
-    double *s_rpt = s_y + T + kWaves * RPW * 6;              // row centroids of the workgroup
+    // per wave: the row lines of up to 64 rows (all its groups when they fit)
+    double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
+    double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
     uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
 
     const int t = threadIdx.x;
@@ -520,34 +521,50 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
     // with `stagger`, concurrently running workgroups sit at different row
     // offsets of their blocks (their stores are not 1 MiB-strided in lockstep)
     const int g_rot = (args.stagger && n_groups > 0) ? (int)(blk % (uint32_t)n_groups) : 0;
+    // group g's geometry: first local row, matrix row, rows, and (stagger >= 2)
+    // the rotation inside a full group -- slot r holds row (r + r_rot) mod RPW
+    auto group_rows = [&](int g, int &xw, int &grow0, int &nrows, int &r_rot) {
+        xw = (g * kWaves + wave) * RPW;
+        grow0 = grow_of(xw);
+        nrows = min(RPW, na - grow0);                          // may be <= 0
+        r_rot = (args.stagger >= 2 && nrows == RPW)
+                    ? (int)((blk * 5u + (uint32_t)g * 3u) & (uint32_t)(RPW - 1)) : 0;
+    };
+    // line of local row xw + row into slot `slot` of the wave's LDS rows
+    auto put_row_line = [&](int slot, int xw, int row, int nrows) {
+        double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+        bool deg = true;
+        if (row < nrows) {
+            x = s_rpt[2 * (xw + row)];
+            y = s_rpt[2 * (xw + row) + 1];
+            deg = row_line(f, x, y, l0, l1, l2);
+        }
+        s_row[wave][slot][0] = l0;
+        s_row[wave][slot][1] = l1;
+        s_row[wave][slot][2] = l2;
+        s_row[wave][slot][3] = x;
+        s_row[wave][slot][4] = y;
+        s_row[wave][slot][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
+    };
+    // all of the wave's groups fit in 64 rows: one lane per row computes every
+    // row line up front (one pass instead of one 16-lane pass per group)
+    const bool pre = RPW * n_groups <= kWave;   // uniform
+    if (pre && lane < RPW * n_groups) {
+        int xw, grow0, nrows, r_rot;
+        const int g = lane / RPW, slot = lane % RPW;
+        group_rows(g, xw, grow0, nrows, r_rot);
+        put_row_line(lane, xw, (slot + r_rot) & (RPW - 1), nrows);
+    }
     for (int g_it = 0; g_it < n_groups; ++g_it) {
         const int g = (g_it + g_rot < n_groups) ? g_it + g_rot : g_it + g_rot - n_groups;
-        const int xw = (g * kWaves + wave) * RPW;             // this wave's first local row
-        const int grow0 = grow_of(xw);                        // ... and matrix row
-        const int nrows = min(RPW, na - grow0);               // scalar, may be <= 0
-        // stagger >= 2 also rotates the row order inside full groups: slot r
-        // holds row (r + r_rot) mod RPW of the group
-        const int r_rot = (args.stagger >= 2 && nrows == RPW)
-                              ? (int)((blk * 5u + (uint32_t)g * 3u) & (uint32_t)(RPW - 1)) : 0;
-        if (lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
-            const int slot = (lane - r_rot) & (RPW - 1);
-            double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
-            bool deg = true;
-            if (lane < nrows) {
-                x = s_rpt[2 * (xw + lane)];
-                y = s_rpt[2 * (xw + lane) + 1];
-                deg = row_line(f, x, y, l0, l1, l2);
-            }
-            s_row[wave][slot][0] = l0;
-            s_row[wave][slot][1] = l1;
-            s_row[wave][slot][2] = l2;
-            s_row[wave][slot][3] = x;
-            s_row[wave][slot][4] = y;
-            s_row[wave][slot][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
-        }
+        int xw, grow0, nrows, r_rot;
+        group_rows(g, xw, grow0, nrows, r_rot);
+        double(*rowp)[6] = s_row[wave] + (pre ? g * RPW : 0);   // this group's slots
+        if (!pre && lane < RPW)   // row lines of this wave's group (wave-private LDS slots)
+            put_row_line((lane - r_rot) & (RPW - 1), xw, lane, nrows);
         // the same wave reads them back (LDS executes one wave's ops in order)
         const bool rows_fast =
-            (nrows == RPW) && __all(lane >= RPW || s_row[wave][lane % RPW][5] == 0.0);
+            (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
 
         Best best[RPW];
 #pragma unroll
@@ -582,9 +599,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     const uint64_t rwrap = rbase + (uint64_t)RPW * rstep;
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        row_fast_lazy<true, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                                s_row[wave][r][2], s_row[wave][r][3],
-                                                s_row[wave][r][4], reinterpret_cast<float *>(rp),
+                        row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1],
+                                                rowp[r][2], rowp[r][3],
+                                                rowp[r][4], reinterpret_cast<float *>(rp),
                                                 jbase, bbits[r], bchunk[r], cidx);
                         rp += rstep;
                         rp = (rp == rwrap) ? rbase : rp;
@@ -593,9 +610,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 } else {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r)
-                        row_fast_lazy<false, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                                 s_row[wave][r][2], s_row[wave][r][3],
-                                                 s_row[wave][r][4], nullptr, jbase, bbits[r],
+                        row_fast_lazy<false, NT>(c, rowp[r][0], rowp[r][1],
+                                                 rowp[r][2], rowp[r][3],
+                                                 rowp[r][4], nullptr, jbase, bbits[r],
                                                  bchunk[r], cidx);
                 }
             }
@@ -617,9 +634,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
             int32_t my_j = 0;
             if (lane < RPW) {   // lane r recovers the column of row slot r
                 const int jj0 = my_c * kChunk + kColsPerLane * my_l;
-                my_j = jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0, s_row[wave][lane][0],
-                                          s_row[wave][lane][1], s_row[wave][lane][2],
-                                          s_row[wave][lane][3], s_row[wave][lane][4], my_k);
+                my_j = jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0, rowp[lane][0],
+                                          rowp[lane][1], rowp[lane][2],
+                                          rowp[lane][3], rowp[lane][4], my_k);
             }
             if (ties) {
 #pragma unroll
@@ -630,9 +647,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     if (bbits[r] == k) {   // every lane holding the minimum finds its first column
                         const int jj0 = bchunk[r] * kChunk + kColsPerLane * lane;
                         cand = (uint32_t)(jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0,
-                                                             s_row[wave][r][0], s_row[wave][r][1],
-                                                             s_row[wave][r][2], s_row[wave][r][3],
-                                                             s_row[wave][r][4], k));
+                                                             rowp[r][0], rowp[r][1],
+                                                             rowp[r][2], rowp[r][3],
+                                                             rowp[r][4], k));
                     }
                     const int32_t jt = (int32_t)wave_min_u32(cand);
                     my_j = (lane == r) ? jt : my_j;
@@ -680,9 +697,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         const int rr = (r + r_rot) & (RPW - 1);
-                        row_fast_strided<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                                 s_row[wave][r][2], s_row[wave][r][3],
-                                                 s_row[wave][r][4],
+                        row_fast_strided<ARGMIN>(c, rowp[r][0], rowp[r][1],
+                                                 rowp[r][2], rowp[r][3],
+                                                 rowp[r][4],
                                                  dbase ? reinterpret_cast<float *>(dbase + (int64_t)(grow0 + rr) * ld)
                                                        : nullptr,
                                                  jbase, best[r]);
@@ -694,8 +711,8 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     for (int r = 0; r < RPW; ++r) {
                         const int rr = (r + r_rot) & (RPW - 1);
                         row_fast<ARGMIN, true, OutT, NT, true>(
-                            c, s_row[wave][r][0], s_row[wave][r][1], s_row[wave][r][2],
-                            s_row[wave][r][3], s_row[wave][r][4],
+                            c, rowp[r][0], rowp[r][1], rowp[r][2],
+                            rowp[r][3], rowp[r][4],
                             reinterpret_cast<OutT *>(rbase + (uint64_t)rr * rstep), jbase, best[r]);
                     }
                 } else if (fast && vec_ok) {   // the common case: clean rows, aligned output
@@ -705,9 +722,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                     const uint64_t rwrap = rbase + (uint64_t)RPW * rstep;
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
-                        row_fast<ARGMIN, true, OutT, NT>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                               s_row[wave][r][2], s_row[wave][r][3],
-                                               s_row[wave][r][4], reinterpret_cast<OutT *>(rp),
+                        row_fast<ARGMIN, true, OutT, NT>(c, rowp[r][0], rowp[r][1],
+                                               rowp[r][2], rowp[r][3],
+                                               rowp[r][4], reinterpret_cast<OutT *>(rp),
                                                jbase, best[r]);
                         rp += rstep;
                         rp = (rp == rwrap) ? rbase : rp;
@@ -719,9 +736,9 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                 } else if (fast && !dbase) {   // association only, no matrix output
 #pragma unroll
                     for (int r = 0; r < RPW; ++r)
-                        row_fast<ARGMIN, false, OutT>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                                      s_row[wave][r][2], s_row[wave][r][3],
-                                                      s_row[wave][r][4], nullptr, jbase, best[r]);
+                        row_fast<ARGMIN, false, OutT>(c, rowp[r][0], rowp[r][1],
+                                                      rowp[r][2], rowp[r][3],
+                                                      rowp[r][4], nullptr, jbase, best[r]);
                 } else {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
@@ -729,10 +746,10 @@ __global__ __launch_bounds__(kThreads) void pairwise_kernel(PairArgs args) {
                             const int rr = (r + r_rot) & (RPW - 1);
                             OutT *drow = dbase ? dbase + (int64_t)(grow0 + rr) * ld : nullptr;
                             const bool rdeg = __builtin_amdgcn_readfirstlane(
-                                                  (int)s_row[wave][r][5]) == (int)kDeg;
-                            row_safe<ARGMIN>(c, s_row[wave][r][0], s_row[wave][r][1],
-                                             s_row[wave][r][2], s_row[wave][r][3],
-                                             s_row[wave][r][4], rdeg, drow, jbase, jstep, best[r]);
+                                                  (int)rowp[r][5]) == (int)kDeg;
+                            row_safe<ARGMIN>(c, rowp[r][0], rowp[r][1],
+                                             rowp[r][2], rowp[r][3],
+                                             rowp[r][4], rdeg, drow, jbase, jstep, best[r]);
                         }
                     }
                 }
@@ -1893,7 +1910,7 @@ constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgrou
 template <int RPW>
 size_t pairwise_lds_bytes(int col_tile, int rows_per_wg) {
     return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
-           (size_t)kWaves * RPW * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double);
+           (size_t)kWaves * kWave * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double);
 }
 
 template <int RPW>
