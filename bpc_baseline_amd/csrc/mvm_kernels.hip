@@ -425,7 +425,8 @@ __device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
 template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
-__global__ __launch_bounds__(kThreads, 3) void pairwise_kernel(PairArgs args) {   // 3 waves/SIMD: <= 168 VGPRs
+// occupancy: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
+__global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(PairArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
     double *s_l0 = reinterpret_cast<double *>(s_dyn);
