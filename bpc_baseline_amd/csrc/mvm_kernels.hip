@@ -119,7 +119,9 @@ __device__ __forceinline__ float value_of_key(uint32_t k) {
 // DPP min step: v = min(v, v from the lane DPP control CTRL selects).
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_min(uint32_t v) {
-    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, 0xF, 0xF, false);
+    // old = UINT_MAX (umin's identity) lets the DPP-combine pass fold the move
+    // into the min (one v_min_u32_dpp per step)
+    const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, 0xF, 0xF, false);
     return o < v ? o : v;
 }
 
