@@ -55,7 +55,14 @@ struct LsapArgs {
     int32_t mid_max_cols;       // long sides in (wave_max_cols, this]: 256-thread lsap_kernel
     unsigned char *sync;        // per-problem barrier + reduction slots (multi kernel)
     int32_t dpp;                // 1: DPP wave reductions in lsap_wave_kernel
+    int32_t lds_max_cols;       // long sides in (wave_max_cols, this]: column state in LDS
+    int32_t lds_small_cols;     // ... of which those up to this: 256-thread LDS kernel
 };
+
+// Column state of lsap_kernel<.., true> in LDS: spc, v (f64), path, row4col,
+// pos, rem (i32) = 32 bytes per long-side column.
+constexpr int kLdsStateBytes = 32;
+constexpr int kLdsMaxCols = 4096;   // 128 KiB + the transpose tile fit the CU's 160 KiB
 
 struct Red {
     double m;      // smallest shortest-path cost seen
@@ -151,9 +158,12 @@ __host__ __device__ inline Layout lsap_layout(int64_t nr, int64_t nc, bool trans
     return L;
 }
 
-template <int NT>
+// LDS: the per-column state lives in LDS instead of the workspace (long
+// sides up to kLdsMaxCols): every Dijkstra scan then reads LDS, not L2/MALL.
+template <int NT, bool LDS = false>
 __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     constexpr int kNW = NT / 64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_state[];
     constexpr int kU = NT >= 1024 ? kScanU : 2 * kScanU;   // batched loads per thread (VGPR budget)
     __shared__ float s_tile[kTile][kTile + 1];
     __shared__ Red s_red[kNW];
@@ -172,18 +182,24 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
     if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
     const int64_t longside = R > K ? R : K;
-    if ((longside <= a.mid_max_cols) != (NT < kLsapThreads)) return;   // the other class
+    // class of the problem: LDS state with 256 threads (long side <= lds_small)
+    // or 1024 threads, then workspace state with 256 or 1024 threads
+    const int cls = longside <= a.lds_max_cols
+                        ? (longside <= a.lds_small_cols ? 0 : 1)
+                        : (longside <= a.mid_max_cols ? 2 : 3);
+    if (cls != (LDS ? 0 : 2) + (NT < kLsapThreads ? 0 : 1)) return;   // another kernel's
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const Layout L = lsap_layout(nr, nc, transpose);
     unsigned char *w = a.ws + a.ws_offs[p];
     const float *C0 = a.cost + a.cost_offs[p];
-    double *spc = reinterpret_cast<double *>(w + L.spc);
-    double *v = reinterpret_cast<double *>(w + L.v);
-    int32_t *path = reinterpret_cast<int32_t *>(w + L.path);
-    int32_t *row4col = reinterpret_cast<int32_t *>(w + L.row4col);
-    int32_t *pos = reinterpret_cast<int32_t *>(w + L.pos);
-    int32_t *rem = reinterpret_cast<int32_t *>(w + L.rem);
+    double *spc = reinterpret_cast<double *>(LDS ? s_state : w + L.spc);
+    double *v = LDS ? spc + nc : reinterpret_cast<double *>(w + L.v);
+    int32_t *path = reinterpret_cast<int32_t *>(LDS ? reinterpret_cast<unsigned char *>(v + nc)
+                                                     : w + L.path);
+    int32_t *row4col = LDS ? path + nc : reinterpret_cast<int32_t *>(w + L.row4col);
+    int32_t *pos = LDS ? row4col + nc : reinterpret_cast<int32_t *>(w + L.pos);
+    int32_t *rem = LDS ? pos + nc : reinterpret_cast<int32_t *>(w + L.rem);
     double *u = reinterpret_cast<double *>(w + L.u);
     int32_t *col4row = reinterpret_cast<int32_t *>(w + L.col4row);
     int32_t *sr = reinterpret_cast<int32_t *>(w + L.sr);
@@ -1051,10 +1067,40 @@ int mvm_lsap_solve_bounded(const float *cost_dev, const int64_t *cost_offs_dev,
     // MI355X: 4096 x 64 problems 4.00 vs 4.36 ms per 1000 with 256 threads;
     // 65536 x 256: 52 vs 80 ms per 200 with 1024 (tools/tune_lsap.py)
     a.mid_max_cols = mvm_env_int("MVM_LSAP_MID_MAX_COLS", 8192);
-    const int64_t lo256 = (int64_t)wave_max + 1, hi256 = a.mid_max_cols;
+    // long sides in (wave_max, MVM_LSAP_LDS_MAX_COLS]: column state in LDS
+    int lds_max = mvm_env_int("MVM_LSAP_LDS_MAX_COLS", kLdsMaxCols);
+    lds_max = lds_max < 0 ? 0 : (lds_max > kLdsMaxCols ? kLdsMaxCols : lds_max);
+    a.lds_max_cols = lds_max > wave_max ? lds_max : 0;
+    a.lds_small_cols = mvm_env_int("MVM_LSAP_LDS_SMALL_COLS", 2048);
+    if (a.multi_g <= 1 && big && a.lds_max_cols > 0) {
+        // dynamic LDS sized for the class's longest side (the batch's when bounded)
+        auto lds_for = [&](int64_t hi) {
+            return (size_t)(long_max < hi ? long_max : hi) * kLdsStateBytes;
+        };
+        const int64_t small_hi = a.lds_small_cols < a.lds_max_cols ? a.lds_small_cols : a.lds_max_cols;
+        if (small_hi > wave_max && overlaps((int64_t)wave_max + 1, small_hi)) {
+            const size_t lds = lds_for(small_hi);
+            if (lds > 64 * 1024 &&
+                hipFuncSetAttribute(reinterpret_cast<const void *>(&lsap_kernel<256, true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+            lsap_kernel<256, true><<<dim3((unsigned)n_problems), dim3(256), lds, s>>>(a);
+        }
+        const int64_t big_lo = (small_hi > wave_max ? small_hi : wave_max) + 1;
+        if (a.lds_max_cols >= big_lo && overlaps(big_lo, a.lds_max_cols)) {
+            const size_t lds = lds_for(a.lds_max_cols);
+            if (lds > 64 * 1024 &&
+                hipFuncSetAttribute(reinterpret_cast<const void *>(&lsap_kernel<kLsapThreads, true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+                return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+            lsap_kernel<kLsapThreads, true><<<dim3((unsigned)n_problems), dim3(kLsapThreads), lds, s>>>(a);
+        }
+    }
+    const int64_t lo256 = (int64_t)(a.lds_max_cols > wave_max ? a.lds_max_cols : wave_max) + 1;
+    const int64_t hi256 = a.mid_max_cols;
     if (!empty_done || (a.multi_g <= 1 && big && overlaps(lo256, hi256)))
         lsap_kernel<256><<<dim3((unsigned)n_problems), dim3(256), 0, s>>>(a);
-    if (a.multi_g <= 1 && big && long_max > (hi256 > wave_max ? hi256 : (int64_t)wave_max))
+    if (a.multi_g <= 1 && big && long_max > (hi256 > lo256 - 1 ? hi256 : lo256 - 1))
         lsap_kernel<kLsapThreads><<<dim3((unsigned)n_problems), dim3(kLsapThreads), 0, s>>>(a);
     return mvm_check_launch("lsap_kernel");
 }

@@ -22,18 +22,25 @@ def _batched(cuda, mats):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-@pytest.fixture(params=["default", "workgroup", "workgroup256", "multi"])
+@pytest.fixture(params=["default", "lds", "workgroup", "workgroup256", "multi"])
 def lsap_path(request, monkeypatch):
-    """default: long sides <= 1024 one problem per wave, larger ones split over
-    co-resident workgroups when the batch leaves room; workgroup: one
-    1024-thread workgroup per problem; multi: every problem split over 4
+    """default: long sides <= 1024 one problem per wave, up to 4096 one
+    workgroup with the column state in LDS, larger ones split over co-resident
+    workgroups when the batch leaves room; lds: every problem of <= 4096 in
+    the LDS-state workgroup; workgroup: one 1024-thread workgroup per problem
+    with the state in the workspace; multi: every problem split over 4
     workgroups."""
-    if request.param == "workgroup":
+    if request.param == "lds":
         monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
         monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+    elif request.param == "workgroup":
+        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
+        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+        monkeypatch.setenv("MVM_LSAP_LDS_MAX_COLS", "0")
     elif request.param == "workgroup256":
         monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
         monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
+        monkeypatch.setenv("MVM_LSAP_LDS_MAX_COLS", "0")
         monkeypatch.setenv("MVM_LSAP_MID_MAX_COLS", "1000000")
     elif request.param == "multi":
         monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
@@ -45,7 +52,8 @@ def test_random_shapes_and_ties_batched(cuda, lsap_path):
     rng = np.random.default_rng(0)
     mats = []
     for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0),
-                  (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70)]:
+                  (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70),
+                  (4096, 6), (6, 4096), (2500, 11), (4097, 3)]:
         for trial in range(4):
             c = rng.normal(size=shape).astype(np.float32)
             if trial == 1:

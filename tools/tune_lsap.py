@@ -21,8 +21,13 @@ ENV = {"wg256": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "1000000"},
        "wg256_shfl": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "1000000", "MVM_LSAP_DPP": "0"},
        "wg1024_shfl": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "0", "MVM_LSAP_DPP": "0"},
        "wave_wg256": {"MVM_LSAP_WAVE_MAX_COLS": "0", "MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "1000000"},
-       "nowave": {"MVM_LSAP_WAVE_MAX_COLS": "0", "MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "0"}}
-KEYS = ("MVM_LSAP_MULTI_G", "MVM_LSAP_MID_MAX_COLS", "MVM_LSAP_WAVE_MAX_COLS", "MVM_LSAP_DPP")
+       "nowave": {"MVM_LSAP_WAVE_MAX_COLS": "0", "MVM_LSAP_MULTI_G": "0", "MVM_LSAP_MID_MAX_COLS": "0"},
+       "lds": {"MVM_LSAP_MULTI_G": "0"},
+       "nolds": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_LDS_MAX_COLS": "0"},
+       "lds1024": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_LDS_SMALL_COLS": "0"},
+       "lds256": {"MVM_LSAP_MULTI_G": "0", "MVM_LSAP_LDS_SMALL_COLS": "4096"}}
+KEYS = ("MVM_LSAP_MULTI_G", "MVM_LSAP_MID_MAX_COLS", "MVM_LSAP_WAVE_MAX_COLS", "MVM_LSAP_DPP",
+        "MVM_LSAP_LDS_MAX_COLS", "MVM_LSAP_LDS_SMALL_COLS")
 dev = torch.device("cuda", 0)
 b = make_scenes(args.scenes, 3, args.dets, seed=1)
 tp = ops.TripletPlan(b.cam_offs, b.n_scenes, device=dev)
