@@ -421,6 +421,83 @@ __device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_
     return q;
 }
 
+// ---- transposed lazy reduction (lazy == 2, the default) ----
+// Minimum over the LPR = 64 / RPW consecutive lanes that share one row slot.
+// Quad xor steps, then row_half_mirror / row_mirror: every lane of the group
+// ends with the group minimum.
+template <int RPW>
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t v) {
+    constexpr int LPR = kWave / RPW;
+    if constexpr (LPR >= 2) v = dpp_min<0xB1>(v);
+    if constexpr (LPR >= 4) v = dpp_min<0x4E>(v);
+    if constexpr (LPR >= 8) v = dpp_min<0x141>(v);
+    if constexpr (LPR >= 16) v = dpp_min<0x140>(v);
+    return v;
+}
+
+// The RPW lane minima of row slot `rs` that segment `seg` owns, from the
+// wave's [RPW][64] LDS scratch (16-byte reads; RPW is a multiple of 4).
+template <int RPW>
+__device__ __forceinline__ void read_segment(const uint32_t *red, int rs, int seg,
+                                             uint32_t (&v)[RPW]) {
+    const uint32_t *src = red + rs * kWave + seg * RPW;
+#pragma unroll
+    for (int i = 0; i < RPW; i += 4) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(src + i);
+        v[i] = q.x;
+        v[i + 1] = q.y;
+        v[i + 2] = q.z;
+        v[i + 3] = q.w;
+    }
+}
+
+// End of a clean (lazy) row group.  Lane L holds, per row slot r, the float32
+// bits of its minimum bbits[r] and the chunk it first reached it in,
+// bchunk[r].  The per-row wave reductions (RPW x (4 DPP + 4 readlane + ballot
+// + selects)) become one transpose through LDS: lane L takes row slot
+// rs = L / LPR and the RPW lanes [seg*RPW, seg*RPW + RPW) of that row
+// (seg = L % LPR), reduces them in registers, and finishes over its LPR lanes
+// with DPP.  The winner is the lowest (chunk, lane) holding the row minimum k
+// -- the lowest column, since column = chunk*256 + 4*lane + q.  Returns k and
+// the winner's lane and chunk, uniform over the LPR lanes of the row slot.
+template <int RPW>
+__device__ __forceinline__ void lazy_reduce_transposed(uint32_t *red, const uint32_t (&bbits)[RPW],
+                                                       const int32_t (&bchunk)[RPW], bool multi,
+                                                       int lane, uint32_t &k, int &w, int &c) {
+    constexpr int LPR = kWave / RPW;
+    const int rs = lane / LPR, seg = lane % LPR;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = bbits[r];
+    // the same wave reads them back: LDS executes one wave's ops in order
+    uint32_t v[RPW];
+    read_segment<RPW>(red, rs, seg, v);
+    uint32_t m = v[0];
+#pragma unroll
+    for (int i = 1; i < RPW; ++i) m = v[i] < m ? v[i] : m;
+    k = group_min_u32<RPW>(m);
+    uint32_t key = 0xFFFFFFFFu;
+    if (!multi) {   // one chunk: the first lane of the segment holding k
+        uint32_t pos = RPW;
+#pragma unroll
+        for (int i = RPW - 1; i >= 0; --i) pos = (v[i] == k) ? (uint32_t)i : pos;
+        key = (pos < (uint32_t)RPW) ? (uint32_t)(seg * RPW) + pos : key;
+    } else {        // several chunks: lowest (chunk, lane) among the lanes holding k
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = (uint32_t)bchunk[r];
+        uint32_t ch[RPW];
+        read_segment<RPW>(red, rs, seg, ch);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const uint32_t ki = (ch[i] << 6) | (uint32_t)(seg * RPW + i);
+            const uint32_t cand = (v[i] == k) ? ki : 0xFFFFFFFFu;
+            key = cand < key ? cand : key;
+        }
+    }
+    key = group_min_u32<RPW>(key);
+    w = (int)(key & 63u);
+    c = (int)(key >> 6);
+}
+
 // Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair).  The
 // normalised lines of (up to col_tile) columns are computed ONCE per
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
@@ -440,6 +517,8 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
     double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
     double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
     uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
+    // lazy == 2: per wave an [RPW][64] u32 scratch for the transposed reduction
+    uint32_t *s_red = s_cst + T;
 
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
@@ -477,6 +556,9 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
     for (int k = 0; k < 9; ++k) f[k] = args.F[(int64_t)sp * 9 + k];
 
     const int64_t doff = args.dist_offs ? args.dist_offs[sp] : (int64_t)sp * args.mat_stride;
+    // first association row of this matrix, loaded before any store (a vector
+    // load issued after the stores would wait for all of them: vmcnt is in order)
+    const int64_t row_off0 = args.row_offs ? args.row_offs[sp] : 0;
     const int64_t ld = args.ld ? args.ld : nb;
     OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
     const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
@@ -619,6 +701,29 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
                                                  bchunk[r], cidx);
                 }
             }
+            if (args.lazy >= 2) {
+                constexpr int LPR = kWave / RPW;
+                uint32_t k;
+                int w, cw;
+                lazy_reduce_transposed<RPW>(s_red + wave * (RPW * kWave), bbits, bchunk,
+                                            nb > kChunk, lane, k, w, cw);
+                // the LPR lanes of row slot rs recompute the winner's 4 values
+                // (lane seg takes q = seg % 4) and keep the first equal to k
+                const int rs = lane / LPR, q = (lane % LPR) & (kColsPerLane - 1);
+                const int jj = cw * kChunk + kColsPerLane * w + q;
+                const double *rl = rowp[rs];
+                const double d1 = __builtin_fma(s_l1[jj], rl[4], s_l0[jj] * rl[3]) + s_l2[jj];
+                const double d2 = __builtin_fma(rl[1], s_y[jj], rl[0] * s_x[jj]) + rl[2];
+                const uint32_t b =
+                    __float_as_uint((float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2)));
+                const uint32_t qm = group_min_u32<RPW>((b == k) ? (uint32_t)q : 0xFFFFFFFFu);
+                if (lane % LPR == 0) {
+                    const int64_t row = row_off0 + grow0 + ((rs + r_rot) & (RPW - 1));
+                    if (args.argmin) args.argmin[row] = jj - q + (int)qm;
+                    if (args.minval) args.minval[row] = __uint_as_float(k);
+                }
+                continue;
+            }
             // per row: wave minimum, its lane and chunk; lane r gathers row r's
             uint32_t my_k = 0;
             int32_t my_l = 0, my_c = 0;
@@ -659,7 +764,7 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
                 }
             }
             if (lane < nrows) {
-                const int64_t row = args.row_offs[sp] + grow0 + ((lane + r_rot) & (RPW - 1));
+                const int64_t row = row_off0 + grow0 + ((lane + r_rot) & (RPW - 1));
                 if (args.argmin) args.argmin[row] = my_j;
                 if (args.minval) args.minval[row] = __uint_as_float(my_k);
             }
@@ -770,10 +875,10 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
             }
             if (args.lane_results) {
                 store_row_results<RPW>(kmin, imin, nrows, lane, r_rot, args.argmin, args.minval,
-                                       args.row_offs[sp] + grow0);
+                                       row_off0 + grow0);
             } else if (lane == 0) {
                 for (int r = 0; r < nrows; ++r) {
-                    const int64_t row = args.row_offs[sp] + grow0 + ((r + r_rot) & (RPW - 1));
+                    const int64_t row = row_off0 + grow0 + ((r + r_rot) & (RPW - 1));
                     if (args.argmin) args.argmin[row] = (kmin[r] == kKeyInvalid) ? -1 : imin[r];
                     if (args.minval) args.minval[row] = value_of_key(kmin[r]);
                 }
@@ -1911,9 +2016,20 @@ int env_int(const char *name, int dflt) {
 constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 
 template <int RPW>
-size_t pairwise_lds_bytes(int col_tile, int rows_per_wg) {
+size_t pairwise_lds_bytes(int col_tile, int rows_per_wg, bool transposed_reduction) {
     return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
-           (size_t)kWaves * kWave * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double);
+           (size_t)kWaves * kWave * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double) +
+           (transposed_reduction ? (size_t)kWaves * RPW * kWave * sizeof(uint32_t) : 0);
+}
+
+// Launch with `lds` bytes of dynamic LDS (above 64 KiB the kernel must opt in).
+template <typename Kernel>
+void launch_lds(Kernel kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+                const PairArgs &a) {
+    if (lds > 65536)
+        (void)hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    kern<<<grid, block, lds, stream>>>(a);
 }
 
 template <int RPW>
@@ -1924,41 +2040,37 @@ void launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_co
     a.xcd_remap = env_int("MVM_PAIRWISE_XCD", 1);   // MI355X C3: 4.63 vs 4.72 ms per launch
     a.interleave = env_int("MVM_PAIRWISE_INTERLEAVE", 0);
     a.stagger = env_int("MVM_PAIRWISE_STAGGER", 0);
-    a.lazy = env_int("MVM_PAIRWISE_LAZY", 1);
+    // 2: transposed reduction (default); 1: per-row DPP reductions; 0: eager argmin
+    a.lazy = env_int("MVM_PAIRWISE_LAZY", 2);
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
     // MVM_PAIRWISE_LDS_PAD (experiments): unused LDS per workgroup, to cap the
     // resident workgroups per CU
-    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg) +
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg,
+                                               argmin && !f64 && a.lazy >= 2) +
                        (size_t)max(0, env_int("MVM_PAIRWISE_LDS_PAD", 0));
-    if (lds > 65536) {
-        const void *fns[] = {reinterpret_cast<const void *>(&pairwise_kernel<RPW, true, float, 1>),
-                             reinterpret_cast<const void *>(&pairwise_kernel<RPW, false, float, 1>)};
-        for (const void *fn : fns)
-            (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    }
     if (f64) {
-        pairwise_kernel<RPW, false, double><<<grid, block, lds, stream>>>(a);
+        launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
     } else {
         // nontemporal stores for whole-line rows; rows that end mid-line share
         // that line with the next row, and L2 must merge it (default policy)
         switch (env_int("MVM_PAIRWISE_NT", (max_cols % 32 == 0) ? 1 : 0)) {
         case 0:
-            if (argmin) pairwise_kernel<RPW, true, float, 0><<<grid, block, lds, stream>>>(a);
-            else pairwise_kernel<RPW, false, float, 0><<<grid, block, lds, stream>>>(a);
+            if (argmin) launch_lds(pairwise_kernel<RPW, true, float, 0>, grid, block, lds, stream, a);
+            else launch_lds(pairwise_kernel<RPW, false, float, 0>, grid, block, lds, stream, a);
             break;
         case 2:
-            if (argmin) pairwise_kernel<RPW, true, float, 2><<<grid, block, lds, stream>>>(a);
-            else pairwise_kernel<RPW, false, float, 2><<<grid, block, lds, stream>>>(a);
+            if (argmin) launch_lds(pairwise_kernel<RPW, true, float, 2>, grid, block, lds, stream, a);
+            else launch_lds(pairwise_kernel<RPW, false, float, 2>, grid, block, lds, stream, a);
             break;
         case 3:
-            if (argmin) pairwise_kernel<RPW, true, float, 3><<<grid, block, lds, stream>>>(a);
-            else pairwise_kernel<RPW, false, float, 3><<<grid, block, lds, stream>>>(a);
+            if (argmin) launch_lds(pairwise_kernel<RPW, true, float, 3>, grid, block, lds, stream, a);
+            else launch_lds(pairwise_kernel<RPW, false, float, 3>, grid, block, lds, stream, a);
             break;
         default:
-            if (argmin) pairwise_kernel<RPW, true, float, 1><<<grid, block, lds, stream>>>(a);
-            else pairwise_kernel<RPW, false, float, 1><<<grid, block, lds, stream>>>(a);
+            if (argmin) launch_lds(pairwise_kernel<RPW, true, float, 1>, grid, block, lds, stream, a);
+            else launch_lds(pairwise_kernel<RPW, false, float, 1>, grid, block, lds, stream, a);
             break;
         }
     }

@@ -47,11 +47,13 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
 
 
 # ----------------------------------------------------------- pairwise ----
-@pytest.fixture(params=["lazy", "eager"])
+@pytest.fixture(params=["lazy_t", "lazy", "eager"])
 def argmin_path(request, monkeypatch):
-    """Run a pairwise test through both argmin paths: the lazy one (clean row
-    groups: per-chunk minimum, column recovered per group) and the eager one."""
-    monkeypatch.setenv("MVM_PAIRWISE_LAZY", "1" if request.param == "lazy" else "0")
+    """Run a pairwise test through every argmin path: the lazy one (clean row
+    groups: per-chunk minimum, column recovered per group) with its transposed
+    LDS reduction (the default) and with per-row DPP reductions, and the
+    eager one."""
+    monkeypatch.setenv("MVM_PAIRWISE_LAZY", {"lazy_t": "2", "lazy": "1", "eager": "0"}[request.param])
     return request.param
 
 

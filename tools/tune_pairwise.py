@@ -49,7 +49,7 @@ for rnd in range(args.rounds + 1):
         lazy, _, pad = lazy.partition(":")
         os.environ["MVM_PAIRWISE_LDS_PAD"] = pad or "0"
         os.environ["MVM_PAIRWISE_STAGGER"] = stg or "0"
-        os.environ["MVM_PAIRWISE_LAZY"] = lazy or "1"
+        os.environ["MVM_PAIRWISE_LAZY"] = lazy or "2"
         os.environ["MVM_PAIRWISE_INTERLEAVE"] = ilv or "0"
         os.environ["MVM_PAIRWISE_LANE_RESULTS"] = lr or "1"
         os.environ["MVM_PAIRWISE_NT"] = nt or "1"
