@@ -503,9 +503,13 @@ __device__ __forceinline__ void lazy_reduce_transposed(uint32_t *red, const uint
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
+// occupancy: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below;
+// -DMVM_PAIRWISE_WAVES16=4 builds the RPW-16 form at 4 (A/B builds only)
+#ifndef MVM_PAIRWISE_WAVES16
+#define MVM_PAIRWISE_WAVES16 3
+#endif
 template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
-// occupancy: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
-__global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(PairArgs args) {
+__global__ __launch_bounds__(kThreads, RPW >= 16 ? MVM_PAIRWISE_WAVES16 : 4) void pairwise_kernel(PairArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
     double *s_l0 = reinterpret_cast<double *>(s_dyn);

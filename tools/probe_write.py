@@ -5,7 +5,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def one():
     import torch
     from bpc_baseline_amd import ops
-    buf = torch.empty(1 << 30, dtype=torch.float32, device="cuda")
+    # MVM_PROBE_ELEMS: buffer size in float32s (default 1 GiElem = 4 GiB)
+    buf = torch.empty(int(os.environ.get("MVM_PROBE_ELEMS", 1 << 30)), dtype=torch.float32, device="cuda")
     for _ in range(3):
         ops.hbm_write_probe(buf)
     torch.cuda.synchronize()
@@ -20,6 +21,7 @@ def one():
                       "lds": os.environ.get("MVM_PROBE_LDS", ""),
                       "rpw": os.environ.get("MVM_PROBE_RPW", ""), "rg": os.environ.get("MVM_PROBE_RG", ""),
                       "pace": os.environ.get("MVM_PROBE_PACE", ""),
+                      "bytes": buf.numel() * 4, "ms": t * 1e3,
                       "TB/s": buf.numel() * 4 / t / 1e12}))
 
 if __name__ == "__main__":
