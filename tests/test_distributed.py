@@ -109,3 +109,27 @@ def test_bench_rccl_process_group_single_rank(tmp_path):
     assert line["gather_check"] == "rank-0 rows equal after gather"
     assert line["parity"].startswith("bit-exact")
     assert "nccl" in line["config"]["parallelism"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("workload", ["c3", "c2cube"])
+def test_bench_graph_replay_single_gpu(tmp_path, workload):
+    """bench.py's single-GPU step as one hipGraph replay: the captured launches
+    run on every replay (the last launch's outputs are bit-exact vs the oracle)
+    and the per-launch event average covers every launch of the step."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("MVM_DIST_FORCE", None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", workload,
+                        "--scenes", "24", "--chunk", "8", "--steps", "2", "--warmup", "1",
+                        "--cpu-seconds", "0", "--graph", "on"],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["parity"].startswith("bit-exact")
+    assert line["config"]["launch"].startswith("one hipGraph replay")
+    assert line["config"]["launches_per_step"] == 3
+    assert line["roofline"]["avg_launch_ms"] > 0
