@@ -25,7 +25,7 @@ Results equal, capture by capture, the reference's ``_match`` outputs fed with
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Iterable, Iterator, List, Optional, Sequence
 
 import numpy as np
 import torch
@@ -33,7 +33,8 @@ import torch
 from .. import ops
 from .utils.camera_utils import camera_pairs, fundamental_matrices_batched
 
-__all__ = ["MatchBatch", "match_captures", "projection_matrices", "rig_matrices"]
+__all__ = ["MatchBatch", "match_capture_stream", "match_captures", "projection_matrices",
+           "rig_matrices"]
 
 
 def projection_matrices(Ks: np.ndarray, RTs: np.ndarray) -> np.ndarray:
@@ -184,3 +185,39 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     return MatchBatch(match=match, cost=cost, X=X, count=count_h,
                       offs=lplan.out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
                       cube=cube if keep_cube else None)
+
+
+def _rig_host(batch: Sequence):
+    """F and P of one ``match_capture_stream`` batch on the host (numpy)."""
+    boxes, conf, cls, img_offs, Ks, RTs = batch
+    S = (int(img_offs.numel()) - 1) // 3
+    return rig_matrices(np.asarray(Ks, dtype=np.float32).reshape(S, 3, 3, 3),
+                        np.asarray(RTs, dtype=np.float64).reshape(S, 3, 4, 4))
+
+
+def match_capture_stream(batches: Iterable[Sequence], **kwargs) -> Iterator[MatchBatch]:
+    """``match_captures`` over a sequence of batches, pipelined: the host F and
+    P of batch b+1 (``rig_matrices``, numpy) are computed on a worker thread
+    while batch b's device chain runs and the main thread waits on its two
+    device->host copies.  Each batch is ``(boxes, conf, cls, img_offs, Ks,
+    RTs)`` as ``match_captures`` takes them; ``kwargs`` are passed through
+    (``F`` / ``proj`` are computed here).  Results equal ``match_captures`` on
+    each batch: the same F and P arithmetic, only earlier.
+    """
+    from concurrent.futures import ThreadPoolExecutor
+    if "F" in kwargs or "proj" in kwargs:
+        raise TypeError("match_capture_stream computes F and proj itself")
+    it = iter(batches)
+    cur = next(it, None)
+    if cur is None:
+        return
+    with ThreadPoolExecutor(max_workers=1) as pool:
+        fut = pool.submit(_rig_host, cur)
+        while cur is not None:
+            nxt = next(it, None)
+            fut_next = pool.submit(_rig_host, nxt) if nxt is not None else None
+            F_h, P_h = fut.result()
+            dev = cur[0].device
+            yield match_captures(*cur, F=torch.from_numpy(F_h).to(dev),
+                                 proj=torch.from_numpy(P_h).to(dev), **kwargs)
+            cur, fut = nxt, fut_next

@@ -117,6 +117,31 @@ def test_batch_vs_oracle_synthetic(cuda):
         assert torch.equal(res2.X[o:o + k], res.X[o:o + k])
 
 
+def test_capture_stream_equals_per_batch(cuda):
+    """match_capture_stream (host F/P of batch b+1 on a worker thread) gives
+    each batch exactly what match_captures gives it; an empty stream yields
+    nothing."""
+    from bpc_baseline_amd.inference.batch_match import match_capture_stream, match_captures
+    from bpc_baseline_amd.synth import make_detector_batch
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    batches = []
+    for seed, (S, n) in enumerate(((40, 12), (7, 30), (25, 5))):
+        b = make_detector_batch(S, n, seed=seed)
+        batches.append((t(b.boxes), t(b.conf), t(b.cls), t(b.img_offs), b.Ks, b.RTs))
+    got = list(match_capture_stream(iter(batches), matching_threshold=30))
+    assert len(got) == len(batches)
+    for bt, r in zip(batches, got):
+        ref = match_captures(*bt, matching_threshold=30)
+        assert np.array_equal(r.count, ref.count) and np.array_equal(r.offs, ref.offs)
+        for s in range(len(r.count)):
+            o, k = int(r.offs[s]), int(r.count[s])
+            assert torch.equal(r.match[o:o + k], ref.match[o:o + k])
+            assert torch.equal(r.X[o:o + k], ref.X[o:o + k])
+    assert list(match_capture_stream([])) == []
+    with pytest.raises(TypeError):
+        next(match_capture_stream(batches, F=None))
+
+
 def test_batch_threshold_inf_and_empty(cuda, golden):
     """threshold=inf keeps every assignment; an all-empty batch is a no-op."""
     z = golden("a3_cost_cubes.npz")

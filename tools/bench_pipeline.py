@@ -14,7 +14,7 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from bpc_baseline_amd.inference.batch_match import match_captures  # noqa: E402
+from bpc_baseline_amd.inference.batch_match import match_capture_stream, match_captures  # noqa: E402
 from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs, fundamental_matrices  # noqa: E402
 from bpc_baseline_amd.synth import make_detector_batch  # noqa: E402
 
@@ -77,6 +77,22 @@ def main():
         match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, F=Fd, proj=Pd)
     torch.cuda.synchronize()
     dt_cached = (time.perf_counter() - t0) / args.steps
+    # the same batches through the pipelined stream (host F/P of batch b+1
+    # on a worker thread while batch b runs on the device)
+    batches = [(boxes, conf, cls, offs, b.Ks, b.RTs)] * args.steps
+    for _ in match_capture_stream(batches[:2]):
+        pass
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in match_capture_stream(batches):
+        res_stream = r
+    torch.cuda.synchronize()
+    dt_stream = (time.perf_counter() - t0) / args.steps
+    assert np.array_equal(res_stream.count, res.count)
+    ms, mr = res_stream.match.cpu().numpy(), res.match.cpu().numpy()
+    for s in range(args.captures):   # rows past count[s] are unused capacity
+        o, k = int(res.offs[s]), int(res.count[s])
+        assert np.array_equal(ms[o:o + k], mr[o:o + k]), s
     stages = {}
     for _ in range(args.steps):
         match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, timings=stages)
@@ -104,6 +120,9 @@ def main():
                    "captures_per_rig": args.rig_group},
         "matches": int(res.count.sum()), "parity_checked": len(check),
         "stage_ms_synchronised": stages,
+        "stream": {"value": args.captures / dt_stream, "ms_per_batch": dt_stream * 1e3,
+                   "note": "match_capture_stream: host F/P of the next batch overlapped with "
+                           "this batch's device chain"},
         "static_rig": {"value": args.captures / dt_cached, "ms_per_batch": dt_cached * 1e3,
                        "note": "F and P computed once and passed in (fixed camera rig)"},
         "cpu_chain": {"value": cpu, "unit": "captures/s", "cores": 1, "kind": "port",
