@@ -26,6 +26,8 @@
 //     reduced across the wave once per row at the end.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <math.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -997,7 +999,8 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
 }
 
 // ------------------------------------------------- fast triplet kernel ----
-// float32(RN(x / 3)) for x >= +0 without an IEEE division in the common case.
+// float32(RN(x / 3)) for x >= +0 without an IEEE division in the common case
+// (third_fast_ok: the -DMVM_CUBE_THIRD_CHECK=1 form; the default is third_q below).
 // q0 = RN(x * RN(1/3)) is within one ulp of RN(x / 3) (RN(1/3) = (1 - 2^-54)/3,
 // so |x*RN(1/3) - x/3| <= ulp/2, plus the product's own rounding).  Their
 // float32 roundings can differ only if a float32 rounding midpoint -- an fp64
@@ -1006,6 +1009,8 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
 // take the correctly rounded division; tests/test_host_logic.py checks the
 // rule on random and adversarial near-midpoint inputs.
 constexpr double kThird = 1.0 / 3.0;
+// residual bound under which a sum of three is finite (tile-wide fast path)
+constexpr double kTameResidual = 0x1p1020;
 
 // 4 consecutive doubles at a 16-byte aligned address (two dwordx4 loads);
 // lanes past the view's end read zeros.
@@ -1030,6 +1035,37 @@ __device__ __forceinline__ bool third_fast_ok(double q0) {
     const bool near_mid = (low29 - ((1u << 28) - 3u)) <= 6u;      // |low29 - 2^28| <= 3
     const bool in_range = ((hi >> 20) - (1023u - 126u)) <= 252u;   // 2^-126 <= q0 < 2^127
     return !near_mid && in_range;                                  // NaN/inf/negative: false
+}
+
+// RN(s / 3) by one Markstein correction (the default): with y = RN(1/3) and
+// q0 = RN(s * y) within one ulp of s/3, r = fma(-q0, 3, s) is exact and
+// q1 = fma(r, y, q0) is the correctly rounded quotient -- for every finite s
+// (checked against the IEEE division on 1.1e9 random, binade-edge,
+// subnormal and near-midpoint inputs, tools/probes/third_markstein.c, and in
+// tests/test_host_logic.py).  Three fp64 ops and a finiteness test instead
+// of the product plus third_fast_ok's midpoint/range test (~8 ops); only
+// non-finite sums (inf: q1 = NaN) take the division.  A sum of residuals is
+// never -0, the one input whose sign the correction would not keep.
+// -DMVM_CUBE_THIRD_CHECK=1 restores the product + third_fast_ok form (A/B).
+#ifndef MVM_CUBE_THIRD_CHECK
+#define MVM_CUBE_THIRD_CHECK 0
+#endif
+__device__ __forceinline__ double third_q(double s) {
+#if MVM_CUBE_THIRD_CHECK
+    return s * kThird;
+#else
+    const double q0 = s * kThird;
+    return __builtin_fma(__builtin_fma(-q0, 3.0, s), kThird, q0);
+#endif
+}
+
+// true: third_q(s) == RN(s / 3); false: the caller divides
+__device__ __forceinline__ bool third_ok(double q) {
+#if MVM_CUBE_THIRD_CHECK
+    return third_fast_ok(q);
+#else
+    return __builtin_isfinite(q);
+#endif
 }
 
 // ------------------------------------------- tiled triplet kernel (v3) ----
@@ -1135,8 +1171,8 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
 #pragma unroll
             for (int q = 0; q < kColsPerLane; ++q) {
                 sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
-                q0[q] = sum[q] * kThird;
-                ok &= third_fast_ok(q0[q]);
+                q0[q] = third_q(sum[q]);
+                ok &= third_ok(q0[q]);
             }
             float v[kColsPerLane];
             const int64_t row = (int64_t)i * M + j0 + r;
@@ -1161,7 +1197,7 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
                 if (!__all(ok || !act)) {
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q)
-                        qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                        qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
                 }
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
@@ -1227,7 +1263,7 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 }
 
 template <int kCubeIB, int kCubeRPW>
-__global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs args) {
+__global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
     __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
     __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
@@ -1304,6 +1340,7 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
     }
     __syncthreads();
     // ---- prologue 2: the tile's pair residuals (row_safe's arithmetic) -------
+    bool tame_in = true;   // every residual this thread produced is <= kTameResidual
     {
         const int k = t;                                   // kThreads == kChunk: one column each
         if (k < P) {
@@ -1313,17 +1350,22 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
             LineRec cl{0.0, 0.0, 0.0, 0.0};
             cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
 #pragma unroll 4
-            for (int r = 0; r < kCubeIB; ++r)
-                s13[r][k] = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+            for (int r = 0; r < kCubeIB; ++r) {
+                const double e = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+                s13[r][k] = e;
+                tame_in &= e <= kTameResidual;
+            }
         } else {
             for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
         }
     }
     for (int x = t; x < kCubeIB * kJ; x += kThreads) {
         const int r = x / kJ, jj = x % kJ;
-        s12[r][jj] = (r < ni && jw0 + jj < M)
-                         ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
-                         : 0.0;
+        const double e = (r < ni && jw0 + jj < M)
+                             ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                             : 0.0;
+        s12[r][jj] = e;
+        tame_in &= e <= kTameResidual;
     }
     double a23[kCubeRPW][kColsPerLane];
     {
@@ -1344,85 +1386,94 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_kernel(CubeFusedArgs a
                 a23[r][q] = (r < nrows && q < kvalid)
                                 ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
                                 : 0.0;
+                tame_in &= a23[r][q] <= kTameResidual;
             }
         }
     }
-    __syncthreads();
+    // every sum of the tile is finite when its three residuals are <= 2^1020
+    // (NaN fails the compare): then third_q is RN(s/3) for all of them and the
+    // main loop needs no per-row check (a loop without the fallback path)
+    const bool tile_fast = __syncthreads_and(tame_in) != 0 && full && !MVM_CUBE_THIRD_CHECK;
     if (nrows <= 0) return;   // after the barrier: no more barriers below
 
-    for (int ii = 0; ii < ni; ++ii) {
-        const int i = i0 + ii;
-        double a13[kColsPerLane];
-        {
-            const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
-            const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
-            a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
-        }
-        uint32_t key[kCubeRPW];
-        int32_t idx[kCubeRPW];
-#pragma unroll
-        for (int r = 0; r < kCubeRPW; ++r) {
-            key[r] = kKeyInvalid;
-            idx[r] = 0x7FFFFFFF;
-            if (r >= nrows) continue;   // uniform
-            const double v12 = s12[ii][wave * kCubeRPW + r];
-            double sum[kColsPerLane], q0[kColsPerLane];
-            bool ok = true;
-#pragma unroll
-            for (int q = 0; q < kColsPerLane; ++q) {
-                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
-                q0[q] = sum[q] * kThird;
-                ok &= third_fast_ok(q0[q]);
+    auto main_loop = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        for (int ii = 0; ii < ni; ++ii) {
+            const int i = i0 + ii;
+            double a13[kColsPerLane];
+            {
+                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
             }
-            float v[kColsPerLane];
-            const int64_t row = (int64_t)i * M + j0 + r;
-            if (full && __all(ok || !act)) {
+            uint32_t key[kCubeRPW];
+            int32_t idx[kCubeRPW];
 #pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                if (act) {
-                    store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                  (uint32_t)kb * 4u, v);
-                }
-                Best b{v[0], kb};
-#pragma unroll
-                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
-                idx[r] = act ? b.j : 0x7FFFFFFF;
-            } else {
-                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
-                // the IEEE division only when some lane needs it (uniform branch)
-                double qq[kColsPerLane];
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
-                if (!__all(ok || !act)) {
-#pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q)
-                        qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                }
+            for (int r = 0; r < kCubeRPW; ++r) {
+                key[r] = kKeyInvalid;
+                idx[r] = 0x7FFFFFFF;
+                if (r >= nrows) continue;   // uniform
+                const double v12 = s12[ii][wave * kCubeRPW + r];
+                double sum[kColsPerLane], q0[kColsPerLane];
+                bool ok = true;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-                    v[q] = (float)qq[q];
-                    if (q < kvalid) {
-                        if (args.cube)
-                            args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
-                        best_update_safe(b, v[q], kb + q);
-                    }
+                    sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                    q0[q] = third_q(sum[q]);
+                    if (!FAST) ok &= third_ok(q0[q]);
                 }
-                key[r] = best_key(b);
-                idx[r] = b.j;
-            }
-        }
-        uint32_t kmin[kCubeRPW];
-        int32_t imin[kCubeRPW];
+                float v[kColsPerLane];
+                const int64_t row = (int64_t)i * M + j0 + r;
+                if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
-        for (int r = 0; r < kCubeRPW; ++r) {
-            kmin[r] = kKeyInvalid;
-            imin[r] = 0;
-            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+                    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                    if (act) {
+                        store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                      (uint32_t)kb * 4u, v);
+                    }
+                    Best b{v[0], kb};
+#pragma unroll
+                    for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                    key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                    idx[r] = act ? b.j : 0x7FFFFFFF;
+                } else {
+                    Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                    // the IEEE division only when some lane needs it (uniform branch)
+                    double qq[kColsPerLane];
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                    if (!__all(ok || !act)) {
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q)
+                            qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) {
+                        v[q] = (float)qq[q];
+                        if (q < kvalid) {
+                            if (args.cube)
+                                args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
+                            best_update_safe(b, v[q], kb + q);
+                        }
+                    }
+                    key[r] = best_key(b);
+                    idx[r] = b.j;
+                }
+            }
+            uint32_t kmin[kCubeRPW];
+            int32_t imin[kCubeRPW];
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                kmin[r] = kKeyInvalid;
+                imin[r] = 0;
+                if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+            }
+            store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
+                                        roff + (int64_t)i * M + j0);
         }
-        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
-                                    roff + (int64_t)i * M + j0);
-    }
+    };
+    if (tile_fast) main_loop(std::integral_constant<bool, true>{});
+    else main_loop(std::integral_constant<bool, false>{});
 }
 
 // ------------------------------------ fused tiled cube, any P (v5) ----
@@ -1588,8 +1639,8 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
                     sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
-                    q0[q] = sum[q] * kThird;
-                    ok &= third_fast_ok(q0[q]);
+                    q0[q] = third_q(sum[q]);
+                    ok &= third_ok(q0[q]);
                 }
                 float v[kColsPerLane];
                 const int64_t row = (int64_t)i * M + j0 + r;
@@ -1614,7 +1665,7 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
                     if (!__all(ok || !act)) {
 #pragma unroll
                         for (int q = 0; q < kColsPerLane; ++q)
-                            qq[q] = third_fast_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                            qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
                     }
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q) {
@@ -1694,8 +1745,8 @@ __host__ __device__ inline size_t small_lds_bytes(int nmax, int ib) {
 
 __device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
     const double sum = (e12 + e13) + e23;
-    const double q0 = sum * kThird;
-    return (float)(third_fast_ok(q0) ? q0 : sum / 3.0);
+    const double q = third_q(sum);
+    return (float)(third_ok(q) ? q : sum / 3.0);
 }
 
 __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {

@@ -1,6 +1,9 @@
 """Host-side logic (CPU): plans, synthetic generator, sharding, input
 validation, the 'no CPU path' contract, and the float32-exactness claim of
 the kernel's exponent-decrement halving."""
+import math
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -197,6 +200,62 @@ def test_fast_division_by_three_rule():
         b = q0.astype(np.float32).view(np.int32)
     assert not np.any((a != b) & ok)
     assert ok[1_000_000:2_000_000].mean() > 0.999   # realistic costs take the fast path
+
+
+def _markstein_third(s: float) -> float:
+    """third_q (mvm_kernels.hip) with exact fma emulation: q0 = RN(s * RN(1/3)),
+    r = fma(-q0, 3, s), q1 = fma(r, RN(1/3), q0).  float(Fraction) and float
+    '/' are correctly rounded in CPython, so each fma is one rounding."""
+    from fractions import Fraction
+    y = 1.0 / 3.0
+    q0 = s * y
+    r = float(Fraction(s) - 3 * Fraction(q0))
+    return float(Fraction(r) * Fraction(y) + Fraction(q0))
+
+
+def test_markstein_division_by_three_is_correctly_rounded():
+    """The cube kernels' default RN(s / 3): one Markstein correction of the
+    product equals the IEEE division bit for bit -- random values over every
+    binade (subnormals included), binade edges, and s next to 3 * (midpoint
+    of two consecutive doubles), where the plain product is most often off."""
+    import struct
+    rng = np.random.default_rng(21)
+    xs = list(rng.integers(1, 0x7FEFFFFFFFFFFFFF, 6000, dtype=np.int64).view(np.float64))
+    xs += list(rng.uniform(0, 30000, 6000)) + [0.0, 3.0, 9999.0, 29997.0, 5e-324, 1.7976931348623157e308]
+    for e in range(-1074, 1024, 7):
+        b = struct.unpack("<q", struct.pack("<d", math.ldexp(1.0, e)))[0]
+        xs += [struct.unpack("<d", struct.pack("<q", b + d))[0] for d in (-1, 0, 1)]
+    for _ in range(3000):
+        e = int(rng.integers(-1000, 1000))
+        k = (1 << 52) | int(rng.integers(0, 1 << 52))
+        s0 = 3.0 * math.ldexp(float(k), e - 52) + math.ldexp(1.5, e - 52)
+        b = struct.unpack("<q", struct.pack("<d", s0))[0]
+        xs += [struct.unpack("<d", struct.pack("<q", b + d))[0] for d in range(-2, 3)]
+    corrected = 0
+    for s in xs:
+        s = float(s)
+        if not (s >= 0.0) or math.isinf(s):
+            continue
+        q1 = _markstein_third(s)
+        assert q1 == s / 3.0 and math.copysign(1.0, q1) == 1.0, s
+        corrected += (s * (1.0 / 3.0)) != s / 3.0
+    assert corrected > 1000          # the plain product is off often enough to matter
+
+
+def test_markstein_division_by_three_c_sweep(tmp_path):
+    """tools/probes/third_markstein.c: the same identity on ~2e7 inputs with the
+    C library's fma (skipped without a C compiler)."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "third_markstein")
+    subprocess.run([cc, "-O2", "-ffp-contract=off", "-o", exe,
+                    os.path.join(repo, "tools", "probes", "third_markstein.c"), "-lm"], check=True)
+    r = subprocess.run([exe, "2000000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout
 
 
 def test_batched_fundamental_matrices_bit_equal():
