@@ -1486,7 +1486,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
 // a chunk's wave minimum replaces the running one only if strictly smaller,
 // so the earliest chunk wins ties (np.argmin's first index).
 template <int kCubeIB, int kCubeRPW>
-__global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFusedArgs args) {
+__global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(CubeFusedArgs args) {
     constexpr int kJ = kWaves * kCubeRPW;
     constexpr int kRows = kCubeIB * kCubeRPW;                                      // (i, j) rows per wave
     constexpr int kSlots = (kRows + kWave - 1) / kWave;
@@ -1560,11 +1560,14 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
         s_p1[jj][1] = py;
     }
     __syncthreads();
+    bool tame12 = true;   // as triplet_fused_kernel's tame_in, for this thread's e12
     for (int x = t; x < kCubeIB * kJ; x += kThreads) {
         const int r = x / kJ, jj = x % kJ;
-        s12[r][jj] = (r < ni && jw0 + jj < M)
-                         ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
-                         : 0.0;
+        const double e = (r < ni && jw0 + jj < M)
+                             ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                             : 0.0;
+        s12[r][jj] = e;
+        tame12 &= e <= kTameResidual;
     }
     uint32_t run_k[kSlots];
     int32_t run_i[kSlots];
@@ -1578,6 +1581,7 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
         const int Pc = min(kChunk, P - kc);
         const int kvalid = Pc - kb;
         if (kc > 0) __syncthreads();   // every wave is done with the previous chunk's s13
+        bool tame_in = tame12;
         {   // e13 of this chunk: one column per thread
             const int k = t;
             double f13[9];
@@ -1587,8 +1591,11 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
                 LineRec cl{0.0, 0.0, 0.0, 0.0};
                 cl.deg = col_line(f13, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
 #pragma unroll 4
-                for (int r = 0; r < kCubeIB; ++r)
-                    s13[r][k] = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+                for (int r = 0; r < kCubeIB; ++r) {
+                    const double e = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+                    s13[r][k] = e;
+                    tame_in &= e <= kTameResidual;
+                }
             } else {
                 for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
             }
@@ -1611,92 +1618,99 @@ __global__ __launch_bounds__(kThreads) void triplet_fused_chunked_kernel(CubeFus
                 a23[r][q] = (r < nrows && q < kvalid)
                                 ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
                                 : 0.0;
+                tame_in &= a23[r][q] <= kTameResidual;
             }
         }
-        __syncthreads();
+        const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+        // every sum of this chunk finite: the loop without the per-row vote
+        const bool chunk_fast = __syncthreads_and(tame_in) != 0 && full && !MVM_CUBE_THIRD_CHECK;
         if (nrows <= 0) continue;   // uniform; the barriers above are still reached
 
-        const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
         const bool act = kvalid > 0;
-        for (int ii = 0; ii < ni; ++ii) {
-            const int i = i0 + ii;
-            double a13[kColsPerLane];
-            {
-                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
-                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
-                a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
-            }
-            uint32_t key[kCubeRPW];
-            int32_t idx[kCubeRPW];
-#pragma unroll
-            for (int r = 0; r < kCubeRPW; ++r) {
-                key[r] = kKeyInvalid;
-                idx[r] = 0x7FFFFFFF;
-                if (r >= nrows) continue;   // uniform
-                const double v12 = s12[ii][wave * kCubeRPW + r];
-                double sum[kColsPerLane], q0[kColsPerLane];
-                bool ok = true;
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
-                    sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
-                    q0[q] = third_q(sum[q]);
-                    ok &= third_ok(q0[q]);
+        auto chunk_loop = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            for (int ii = 0; ii < ni; ++ii) {
+                const int i = i0 + ii;
+                double a13[kColsPerLane];
+                {
+                    const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                    const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                    a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
                 }
-                float v[kColsPerLane];
-                const int64_t row = (int64_t)i * M + j0 + r;
-                if (full && __all(ok || !act)) {
+                uint32_t key[kCubeRPW];
+                int32_t idx[kCubeRPW];
 #pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
-                    if (act) {
-                        store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
-                                      (uint32_t)kb * 4u, v);
-                    }
-                    Best b{v[0], kb};
-#pragma unroll
-                    for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
-                    key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
-                    idx[r] = act ? b.j : 0x7FFFFFFF;
-                } else {
-                    Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
-                    // the IEEE division only when some lane needs it (uniform branch)
-                    double qq[kColsPerLane];
-#pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
-                    if (!__all(ok || !act)) {
-#pragma unroll
-                        for (int q = 0; q < kColsPerLane; ++q)
-                            qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
-                    }
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    key[r] = kKeyInvalid;
+                    idx[r] = 0x7FFFFFFF;
+                    if (r >= nrows) continue;   // uniform
+                    const double v12 = s12[ii][wave * kCubeRPW + r];
+                    double sum[kColsPerLane], q0[kColsPerLane];
+                    bool ok = true;
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q) {
-                        v[q] = (float)qq[q];
-                        if (q < kvalid) {
-                            if (args.cube)
-                                args.cube[coff + row * P + kc + kb + q] = v[q];
-                            best_update_safe(b, v[q], kb + q);
-                        }
+                        sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                        q0[q] = third_q(sum[q]);
+                        if (!FAST) ok &= third_ok(q0[q]);
                     }
-                    key[r] = best_key(b);
-                    idx[r] = b.j;
+                    float v[kColsPerLane];
+                    const int64_t row = (int64_t)i * M + j0 + r;
+                    if (FAST || (full && __all(ok || !act))) {
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                        if (act) {
+                            store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
+                                          (uint32_t)kb * 4u, v);
+                        }
+                        Best b{v[0], kb};
+#pragma unroll
+                        for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                        key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                        idx[r] = act ? b.j : 0x7FFFFFFF;
+                    } else {
+                        Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                        // the IEEE division only when some lane needs it (uniform branch)
+                        double qq[kColsPerLane];
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                        if (!__all(ok || !act)) {
+#pragma unroll
+                            for (int q = 0; q < kColsPerLane; ++q)
+                                qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                        }
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) {
+                            v[q] = (float)qq[q];
+                            if (q < kvalid) {
+                                if (args.cube)
+                                    args.cube[coff + row * P + kc + kb + q] = v[q];
+                                best_update_safe(b, v[q], kb + q);
+                            }
+                        }
+                        key[r] = best_key(b);
+                        idx[r] = b.j;
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    if (r >= nrows) continue;
+                    uint32_t km;
+                    int32_t im;
+                    wave_argmin(key[r], idx[r], km, im);
+                    const int x = ii * kCubeRPW + r;   // uniform
+                    const bool mine = lane == (x % kWave);
+#pragma unroll
+                    for (int z = 0; z < kSlots; ++z) {
+                        if (z != x / kWave) continue;   // uniform
+                        const bool take = mine && km < run_k[z];
+                        run_k[z] = take ? km : run_k[z];
+                        run_i[z] = take ? kc + im : run_i[z];
+                    }
                 }
             }
-#pragma unroll
-            for (int r = 0; r < kCubeRPW; ++r) {
-                if (r >= nrows) continue;
-                uint32_t km;
-                int32_t im;
-                wave_argmin(key[r], idx[r], km, im);
-                const int x = ii * kCubeRPW + r;   // uniform
-                const bool mine = lane == (x % kWave);
-#pragma unroll
-                for (int z = 0; z < kSlots; ++z) {
-                    if (z != x / kWave) continue;   // uniform
-                    const bool take = mine && km < run_k[z];
-                    run_k[z] = take ? km : run_k[z];
-                    run_i[z] = take ? kc + im : run_i[z];
-                }
-            }
-        }
+        };
+        if (chunk_fast) chunk_loop(std::integral_constant<bool, true>{});
+        else chunk_loop(std::integral_constant<bool, false>{});
     }
     if (nrows <= 0) return;
 #pragma unroll
