@@ -1759,8 +1759,13 @@ __host__ __device__ inline size_t small_lds_bytes(int nmax, int ib) {
 
 __device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
     const double sum = (e12 + e13) + e23;
-    const double q = third_q(sum);
-    return (float)(third_ok(q) ? q : sum / 3.0);
+    double q = third_q(sum);
+    if (!third_ok(q)) {   // non-finite sum: the IEEE division, skipped when no lane needs it
+        double s2 = sum;
+        __asm__ volatile("" : "+v"(s2));   // keeps the division inside the branch (no if-conversion)
+        q = s2 / 3.0;
+    }
+    return (float)q;
 }
 
 __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {
