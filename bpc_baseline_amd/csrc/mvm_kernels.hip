@@ -247,6 +247,62 @@ __device__ __forceinline__ void store_row_results(const uint32_t (&kmin)[RPW],
     }
 }
 
+// The partner lane's value under DPP control CTRL (every lane has a partner).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_from(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
+
+// Argmin of 8 rows over the wave when every lane's column indices exceed
+// those of the lanes below it (one k-chunk of the cube: lane l holds columns
+// 4l..4l+3, idx = its first minimum).  A transposing butterfly reduces the 8
+// rows' keys together: after the xor-1/2/4 steps each lane holds one row
+// (r = 4*b0 + 2*b1 + b2 of its lane bits) reduced over its 8-lane group, and
+// the xor-8/16/32 steps finish it -- ~32 VALU for the 8 rows instead of 8
+// per-row DPP chains.  The winner of row r is then the lowest lane holding
+// its minimum (ballot + ff1): the lowest column, np.argmin's rule.  Lane r
+// returns row r's key and index (store_row_results' layout, r_rot = 0).
+template <int N>
+__device__ __forceinline__ void wave_argmin8_transposed(const uint32_t (&key)[N],
+                                                        const int32_t (&idx)[N], int lane,
+                                                        uint32_t &my_k, int32_t &my_i) {
+    static_assert(N == 8, "8 rows");
+    const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4;
+    uint32_t w[4], x[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {   // xor 1: keep rows 4*b0 + i
+        const uint32_t send = b0 ? key[i] : key[i + 4], keep = b0 ? key[i + 4] : key[i];
+        w[i] = umin(keep, dpp_from<0xB1>(send));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {   // xor 2: keep rows 4*b0 + 2*b1 + i
+        const uint32_t send = b1 ? w[i] : w[i + 2], keep = b1 ? w[i + 2] : w[i];
+        x[i] = umin(keep, dpp_from<0x4E>(send));
+    }
+    uint32_t y;
+    {                               // xor 4 (swizzle, bit mode): keep row 4*b0 + 2*b1 + b2
+        const uint32_t send = b2 ? x[0] : x[1], keep = b2 ? x[1] : x[0];
+        y = umin(keep, (uint32_t)__builtin_amdgcn_ds_swizzle((int)send, 0x1F | (4 << 10)));
+    }
+    y = umin(y, dpp_from<0x128>(y));                                                  // xor 8 (row_ror:8)
+    y = umin(y, (uint32_t)__builtin_amdgcn_ds_swizzle((int)y, 0x1F | (16 << 10)));      // xor 16
+    y = umin(y, (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, (int)y));      // xor 32
+    my_k = kKeyInvalid;
+    my_i = 0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        // a lane whose row is r: bits (b0, b1, b2) = (r >> 2, r >> 1, r) & 1
+        const int lr = ((r >> 2) & 1) | (((r >> 1) & 1) << 1) | ((r & 1) << 2);
+        const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)y, lr);
+        const uint64_t hit = __ballot(key[r] == k);
+        const int32_t ix = __builtin_amdgcn_readlane(idx[r], (int)__builtin_ctzll(hit));
+        my_k = (lane == r) ? k : my_k;
+        my_i = (lane == r) ? ix : my_i;
+    }
+}
+
 // 0.5 * s for s >= +0 finite, as bits, EXACT after the float32 cast: the
 // saturating decrement of the exponent field halves every s >= 2^-1021
 // exactly, maps +0 to +0, and maps s < 2^-1021 to some fp64 value below
@@ -1460,16 +1516,27 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     idx[r] = b.j;
                 }
             }
-            uint32_t kmin[kCubeRPW];
-            int32_t imin[kCubeRPW];
+            if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
+                uint32_t mk;
+                int32_t mi;
+                wave_argmin8_transposed(key, idx, lane, mk, mi);
+                if (lane < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                    if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
+                    if (args.minval) args.minval[row] = value_of_key(mk);
+                }
+            } else {
+                uint32_t kmin[kCubeRPW];
+                int32_t imin[kCubeRPW];
 #pragma unroll
-            for (int r = 0; r < kCubeRPW; ++r) {
-                kmin[r] = kKeyInvalid;
-                imin[r] = 0;
-                if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    kmin[r] = kKeyInvalid;
+                    imin[r] = 0;
+                    if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+                }
+                store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
+                                            roff + (int64_t)i * M + j0);
             }
-            store_row_results<kCubeRPW>(kmin, imin, nrows, lane, 0, args.argmin, args.minval,
-                                        roff + (int64_t)i * M + j0);
         }
     };
     if (tile_fast) main_loop(std::integral_constant<bool, true>{});
