@@ -262,12 +262,13 @@ __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b 
 // (r = 4*b0 + 2*b1 + b2 of its lane bits) reduced over its 8-lane group, and
 // the xor-8/16/32 steps finish it -- ~32 VALU for the 8 rows instead of 8
 // per-row DPP chains.  The winner of row r is then the lowest lane holding
-// its minimum (ballot + ff1): the lowest column, np.argmin's rule.  Lane r
-// returns row r's key and index (store_row_results' layout, r_rot = 0).
+// its minimum (ballot + ff1): the lowest column, np.argmin's rule.  Lane
+// dst0 + r returns row r's key and index (dst0 = 0: store_row_results' layout).
 template <int N>
 __device__ __forceinline__ void wave_argmin8_transposed(const uint32_t (&key)[N],
                                                         const int32_t (&idx)[N], int lane,
-                                                        uint32_t &my_k, int32_t &my_i) {
+                                                        uint32_t &my_k, int32_t &my_i,
+                                                        int dst0 = 0) {
     static_assert(N == 8, "8 rows");
     const bool b0 = lane & 1, b1 = lane & 2, b2 = lane & 4;
     uint32_t w[4], x[2];
@@ -298,8 +299,8 @@ __device__ __forceinline__ void wave_argmin8_transposed(const uint32_t (&key)[N]
         const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)y, lr);
         const uint64_t hit = __ballot(key[r] == k);
         const int32_t ix = __builtin_amdgcn_readlane(idx[r], (int)__builtin_ctzll(hit));
-        my_k = (lane == r) ? k : my_k;
-        my_i = (lane == r) ? ix : my_i;
+        my_k = (lane == dst0 + r) ? k : my_k;
+        my_i = (lane == dst0 + r) ? ix : my_i;
     }
 }
 
@@ -1757,6 +1758,22 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
                         key[r] = best_key(b);
                         idx[r] = b.j;
                     }
+                }
+                if constexpr (FAST && kCubeRPW == 8 && kWave % 8 == 0) {
+                    // rows x = ii*8 + r land in lanes x % 64 of slot x / 64 directly
+                    const int x0 = ii * kCubeRPW;   // uniform
+                    uint32_t km;
+                    int32_t im;
+                    wave_argmin8_transposed(key, idx, lane, km, im, x0 % kWave);
+                    const bool mine = lane - x0 % kWave >= 0 && lane - x0 % kWave < nrows;
+#pragma unroll
+                    for (int z = 0; z < kSlots; ++z) {
+                        if (z != x0 / kWave) continue;   // uniform
+                        const bool take = mine && km < run_k[z];
+                        run_k[z] = take ? km : run_k[z];
+                        run_i[z] = take ? kc + im : run_i[z];
+                    }
+                    continue;
                 }
 #pragma unroll
                 for (int r = 0; r < kCubeRPW; ++r) {
