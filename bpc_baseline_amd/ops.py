@@ -32,6 +32,24 @@ __all__ = [
 ]
 
 
+def _h2d_int64(arrays: List[np.ndarray], device: torch.device) -> List[Tensor]:
+    """Host int64 arrays -> device tensors with ONE copy: concatenated into a
+    pinned staging buffer and copied without blocking (a plan's offsets used
+    to cost one synchronous pageable copy each).  Returns views of the one
+    device buffer, in order."""
+    flat = np.concatenate([np.ascontiguousarray(a, dtype=np.int64).reshape(-1) for a in arrays])
+    host = torch.from_numpy(flat)
+    if device.type == "cuda":
+        dev = host.pin_memory().to(device, non_blocking=True)
+    else:
+        dev = host.to(device)
+    out, o = [], 0
+    for a in arrays:
+        out.append(dev[o:o + a.size])
+        o += a.size
+    return out
+
+
 def _p(t: Optional[Tensor]):
     if t is None or t.numel() == 0:
         return None
@@ -301,8 +319,7 @@ class PairwisePlan:
         self.n_rows = int(row_offs[-1])
         self.dist_offs_host, self.row_offs_host = dist_offs, row_offs
         self.device = torch.device(device)
-        self.dist_offs = torch.from_numpy(dist_offs).to(self.device)
-        self.row_offs = torch.from_numpy(row_offs).to(self.device)
+        self.dist_offs, self.row_offs = _h2d_int64([dist_offs, row_offs], self.device)
 
     def matrix(self, dist: Tensor, scene: int, pair: int) -> Tensor:
         """View of the (scene, pair) residual matrix inside a flat ``dist``."""
@@ -359,8 +376,7 @@ class TripletPlan:
         self.n_rows = int(row_offs[-1])
         self.cube_offs_host, self.row_offs_host = cube_offs, row_offs
         self.device = torch.device(device)
-        self.cube_offs = torch.from_numpy(cube_offs).to(self.device)
-        self.row_offs = torch.from_numpy(row_offs).to(self.device)
+        self.cube_offs, self.row_offs = _h2d_int64([cube_offs, row_offs], self.device)
         self.workspace_bytes = int(_native.load().mvm_triplet_workspace_bytes(self.n_scenes,
                                                                                self.max_n))
         self.workspace = torch.empty(max(self.workspace_bytes, 16), dtype=torch.uint8,
@@ -410,9 +426,8 @@ class LsapPlan:
         self.rows, self.cols = rows, cols
         self.out_offs_host = out_offs
         self.device = torch.device(device)
-        self.dims = torch.from_numpy(np.stack([rows, cols], axis=1).reshape(-1).copy()).to(self.device)
-        self.ws_offs = torch.from_numpy(ws_offs).to(self.device)
-        self.out_offs = torch.from_numpy(out_offs).to(self.device)
+        self.dims, self.ws_offs, self.out_offs = _h2d_int64(
+            [np.stack([rows, cols], axis=1).reshape(-1), ws_offs, out_offs], self.device)
         self.workspace = torch.empty(max(int(total), 16), dtype=torch.uint8, device=self.device)
         self.n_out = int(out_offs[-1])
         longs = np.maximum(rows, cols)[(rows > 0) & (cols > 0)]
