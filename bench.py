@@ -468,6 +468,9 @@ def main():
             "traffic": (traffic or {}).get("bytes_per_launch"),
             "bytes_per_launch": float(byts.sum() / n_launch),
             "avg_launch_ms": avg_dur * 1e3,
+            "event_scope": ("one event pair over the timed region: includes the dispatch gap "
+                            "between graph replays" if graph is not None else
+                            "one event pair per launch"),
             "units_per_s_in_kernel": float(units_ev.sum() / durs.sum()),
             "write_probe_gbs": probe_gbs,
             "frac_of_write_probe": (achieved_gbs / probe_gbs) if probe_gbs else None,
