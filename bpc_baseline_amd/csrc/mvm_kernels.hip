@@ -1319,8 +1319,15 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
     for (int q = 0; q < 9; ++q) f[q] = F[q];
 }
 
-template <int kCubeIB, int kCubeRPW>
+// HALF (views of <= 128 detections, kCubeRPW == 8): each half-wave takes
+// one of two (i, j) rows with lanes along k (4 k per lane, 128 k), so a
+// wave instruction covers two rows and no lane idles past P <= 128; a lane
+// computes rows r + 4*(lane / 32) of its wave's 8.  The argmin of the 8 rows
+// is the transposed butterfly over keys that are invalid in the other half.
+template <int kCubeIB, int kCubeRPW, bool HALF = false>
 __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
+    static_assert(!HALF || kCubeRPW == 8, "HALF pairs rows r and r + 4 of 8");
+    constexpr int kLaneRows = HALF ? kCubeRPW / 2 : kCubeRPW;   // rows a lane computes
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
     __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
     __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
@@ -1349,13 +1356,14 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int ni = min(kCubeIB, N - i0);
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
-    const int kb = kColsPerLane * lane;
+    const int hl = HALF ? lane / (kWave / 2) : 0;                  // row half of the lane
+    const int kb = kColsPerLane * (HALF ? lane % (kWave / 2) : lane);
     const int kvalid = P - kb;
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
     // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
     const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
-    const bool act = kvalid > 0;
+    const bool act_k = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
     const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
@@ -1424,7 +1432,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
         s12[r][jj] = e;
         tame_in &= e <= kTameResidual;
     }
-    double a23[kCubeRPW][kColsPerLane];
+    double a23[kLaneRows][kColsPerLane];
     {
         double f[9];
         load_f(F23, f);
@@ -1438,9 +1446,10 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                 cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
             }
 #pragma unroll
-            for (int r = 0; r < kCubeRPW; ++r) {
-                const int jj = wave * kCubeRPW + r;
-                a23[r][q] = (r < nrows && q < kvalid)
+            for (int r = 0; r < kLaneRows; ++r) {
+                const int rr = r + hl * kLaneRows;            // the wave row
+                const int jj = wave * kCubeRPW + rr;
+                a23[r][q] = (rr < nrows && q < kvalid)
                                 ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
                                 : 0.0;
                 tame_in &= a23[r][q] <= kTameResidual;
@@ -1463,14 +1472,16 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                 const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
                 a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
             }
-            uint32_t key[kCubeRPW];
-            int32_t idx[kCubeRPW];
+            uint32_t key[kLaneRows];
+            int32_t idx[kLaneRows];
 #pragma unroll
-            for (int r = 0; r < kCubeRPW; ++r) {
+            for (int r = 0; r < kLaneRows; ++r) {
                 key[r] = kKeyInvalid;
                 idx[r] = 0x7FFFFFFF;
-                if (r >= nrows) continue;   // uniform
-                const double v12 = s12[ii][wave * kCubeRPW + r];
+                if (r >= nrows) continue;   // uniform (the lower half's row is the smaller)
+                const int rr = r + hl * kLaneRows;                 // the wave row
+                const bool act = act_k && rr < nrows;              // HALF: the upper row may not exist
+                const double v12 = s12[ii][wave * kCubeRPW + rr];
                 double sum[kColsPerLane], q0[kColsPerLane];
                 bool ok = true;
 #pragma unroll
@@ -1480,7 +1491,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     if (!FAST) ok &= third_ok(q0[q]);
                 }
                 float v[kColsPerLane];
-                const int64_t row = (int64_t)i * M + j0 + r;
+                const int64_t row = (int64_t)i * M + j0 + rr;
                 if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
@@ -1507,7 +1518,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q) {
                         v[q] = (float)qq[q];
-                        if (q < kvalid) {
+                        if (act && q < kvalid) {
                             if (args.cube)
                                 args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
                             best_update_safe(b, v[q], kb + q);
@@ -1517,7 +1528,24 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     idx[r] = b.j;
                 }
             }
-            if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
+            if constexpr (HALF) {   // rows r and r + 4 share a wave: keys of the other half are invalid
+                uint32_t key8[kCubeRPW];
+                int32_t idx8[kCubeRPW];
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    const bool mine = (r / kLaneRows) == hl;
+                    key8[r] = mine ? key[r % kLaneRows] : kKeyInvalid;
+                    idx8[r] = mine ? idx[r % kLaneRows] : 0x7FFFFFFF;
+                }
+                uint32_t mk;
+                int32_t mi;
+                wave_argmin8_transposed(key8, idx8, lane, mk, mi);
+                if (lane < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                    if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
+                    if (args.minval) args.minval[row] = value_of_key(mk);
+                }
+            } else if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
                 uint32_t mk;
                 int32_t mi;
                 wave_argmin8_transposed(key, idx, lane, mk, mi);
@@ -2515,6 +2543,11 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
             return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                         (long long)blocks);
         const dim3 grid((unsigned)blocks), block(kThreads);
+        // views of <= 128: two rows per wave instruction (MVM_TRIPLET_HALF=0: off)
+        if (tile == 3 && max_n <= kChunk / 2 && env_int("MVM_TRIPLET_HALF", 1)) {
+            triplet_fused_kernel<16, 8, true><<<grid, block, 0, s>>>(c);
+            return check_launch("triplet_fused_kernel");
+        }
         switch (tile) {
         case 4: triplet_fused_kernel<32, 8><<<grid, block, 0, s>>>(c); break;
         case 2: triplet_fused_kernel<8, 8><<<grid, block, 0, s>>>(c); break;

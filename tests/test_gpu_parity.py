@@ -207,7 +207,8 @@ def test_cube_golden_batched(cuda, golden, cube_path):
 @pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False),
                                         (300, 24, False), (40, 64, True), (7, 1, False),
                                         (2, 512, False), (3, 333, True), (1, 770, False), (2, 200, False),
-                                        (2, 384, False)])
+                                        (2, 384, False), (20, 96, False), (6, 100, True), (5, 128, False),
+                                        (9, 77, True), (4, 68, False)])
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
@@ -270,17 +271,19 @@ def test_launches_capture_into_a_hip_graph(cuda):
                            r.view(torch.int32) if r.dtype == torch.float32 else r)
 
 
-def test_cube_row_minimum_ties_across_chunks(cuda, cube_path):
-    """Views of more than 256: a row's winning k duplicated in its own lane
-    group, in the same lane of the next 256-chunk and in the ragged tail chunk;
-    the lowest k must win (the chunked kernel keeps the earliest chunk)."""
+@pytest.mark.parametrize("n", [520, 100])
+def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
+    """A row's winning k duplicated in its own lane group, in another lane and
+    (views of more than 256) in the same lane of the next 256-chunk and in the
+    ragged tail chunk; the lowest k must win (the chunked kernel keeps the
+    earliest chunk).  n = 100 runs the two-rows-per-wave kernel, with rows in
+    both halves of a wave (wave rows 0..3 and 4..7)."""
     from bpc_baseline_amd.synth import make_scenes
-    n = 520
     b = make_scenes(1, 3, n, seed=21)
     pts = b.pts.copy()
     _, ra, _, _, _ = O.cube(pts, b.cam_offs, b.F, 1, want_cube=False)
     o3 = int(b.cam_offs[2])
-    for row in (0, 77):
+    for row in (0, 77, 6 * n + 5):
         k0 = int(ra[row])
         for k in {k0 ^ 1, (k0 + 256) % n, (k0 + 260) % n, n - 3}:
             pts[o3 + k] = pts[o3 + k0]

@@ -35,13 +35,15 @@ env = {"tile": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPL
        "t16x32": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_TILE": "3"},
        "generic": {"MVM_TRIPLET_VARIANT": "1"},
        "chunked": {"MVM_TRIPLET_CHUNKED": "1"},
-       "nochunk": {"MVM_TRIPLET_CHUNKED": "0"}}
+       "nochunk": {"MVM_TRIPLET_CHUNKED": "0"},
+       "nohalf": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_HALF": "0"}}
 times = {v: [] for v in args.variants.split(",")}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in times:
         for k in ("MVM_TRIPLET_RPW", "MVM_TRIPLET_VARIANT", "MVM_TRIPLET_TILE", "MVM_TRIPLET_SMALL",
-                  "MVM_TRIPLET_SMALL_IB", "MVM_TRIPLET_FUSED", "MVM_TRIPLET_XCD", "MVM_TRIPLET_CHUNKED"):
+                  "MVM_TRIPLET_SMALL_IB", "MVM_TRIPLET_FUSED", "MVM_TRIPLET_XCD", "MVM_TRIPLET_CHUNKED",
+                  "MVM_TRIPLET_HALF"):
             os.environ.pop(k, None)
         os.environ.update(env[v])
         ops.triplet_cost_argmin(pts, co, F, plan, out=out)
