@@ -1849,6 +1849,9 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
 // wave instruction 1 KiB contiguous whatever P is -- and finally one thread
 // per (i, j) row recomputes the row from LDS for the argmin over k.
 constexpr int kSmallMaxN = 64;
+// default switch-over to the two-rows-per-wave fused kernel: measured per 1000
+// scenes, small vs fused: 48^3 0.219 vs 0.259 ms, 56^3 0.417 vs 0.344 ms
+constexpr int kSmallAutoMaxN = 52;
 
 struct CubeSmallArgs {
     const double *pts;
@@ -2191,7 +2194,7 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 //   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
 //   MVM_PAIRWISE_NT   row store policy: 1 nt (default), 0 default, 2 sc1, 3 sc0 sc1
-//   MVM_TRIPLET_SMALL 1: one-workgroup-per-scene cube for views of <= 64
+//   MVM_TRIPLET_SMALL one-workgroup-per-scene cube: unset = views of <= 52, 1 = < 64, 0 = off
 //   MVM_TRIPLET_FUSED 1: tiled cube with in-prologue pair residuals (<= 256)
 //   MVM_LSAP_WAVE_MAX_COLS  long-side limit of the one-wave LSAP (mvm_lsap.hip)
 int env_int(const char *name, int dflt) {
@@ -2490,7 +2493,11 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
     const int variant = env_int("MVM_TRIPLET_VARIANT", 3);   // 3 tiled / fused, 1 generic
     // the small kernel up to 63 detections; at 64 the fused tiles are ~10% faster
     // (0.75 vs 0.84 ms per 1000 scenes; below 64 the small kernel wins by 1.1-2.4x)
-    if (max_n < kSmallMaxN && env_int("MVM_TRIPLET_SMALL", 1) && variant == 3) {
+    // MVM_TRIPLET_SMALL: unset = views of <= kSmallAutoMaxN, 1 = up to the
+    // kernel's limit (< kSmallMaxN), 0 = never
+    const int small_env = env_int("MVM_TRIPLET_SMALL", -1);
+    const bool small = small_env < 0 ? max_n <= kSmallAutoMaxN : (small_env != 0 && max_n < kSmallMaxN);
+    if (small && variant == 3) {
         // one workgroup per scene, everything in LDS, no workspace pass
         CubeSmallArgs c{};
         c.pts = pts_dev;
