@@ -1319,15 +1319,18 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
     for (int q = 0; q < 9; ++q) f[q] = F[q];
 }
 
-// HALF (views of <= 128 detections, kCubeRPW == 8): each half-wave takes
-// one of two (i, j) rows with lanes along k (4 k per lane, 128 k), so a
-// wave instruction covers two rows and no lane idles past P <= 128; a lane
-// computes rows r + 4*(lane / 32) of its wave's 8.  The argmin of the 8 rows
-// is the transposed butterfly over keys that are invalid in the other half.
-template <int kCubeIB, int kCubeRPW, bool HALF = false>
+// SPLIT 2 / 4 (views of <= 128 / <= 64 detections, kCubeRPW == 8): the wave
+// splits into SPLIT lane groups of 64/SPLIT lanes, each taking one (i, j) row
+// with lanes along k (4 k per lane), so a wave instruction covers SPLIT rows
+// and no lane idles past P <= 256/SPLIT; a lane computes wave rows
+// r + (8/SPLIT)*(its group).  The argmin of the 8 rows is the transposed
+// butterfly over keys that are invalid outside each row's group.
+template <int kCubeIB, int kCubeRPW, int SPLIT = 1>
 __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
-    static_assert(!HALF || kCubeRPW == 8, "HALF pairs rows r and r + 4 of 8");
-    constexpr int kLaneRows = HALF ? kCubeRPW / 2 : kCubeRPW;   // rows a lane computes
+    constexpr bool HALF = SPLIT > 1;   // split mapping
+    static_assert(SPLIT == 1 || (kCubeRPW == 8 && (SPLIT == 2 || SPLIT == 4)), "8 rows in 2 or 4 groups");
+    constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
+    constexpr int kLPR = kWave / SPLIT;           // lanes per row
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
     __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
     __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
@@ -1356,8 +1359,8 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int ni = min(kCubeIB, N - i0);
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
-    const int hl = HALF ? lane / (kWave / 2) : 0;                  // row half of the lane
-    const int kb = kColsPerLane * (HALF ? lane % (kWave / 2) : lane);
+    const int hl = lane / kLPR;                                      // row group of the lane
+    const int kb = kColsPerLane * (lane % kLPR);
     const int kvalid = P - kb;
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
@@ -1528,7 +1531,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     idx[r] = b.j;
                 }
             }
-            if constexpr (HALF) {   // rows r and r + 4 share a wave: keys of the other half are invalid
+            if constexpr (HALF) {   // SPLIT rows share a wave: keys of the other groups are invalid
                 uint32_t key8[kCubeRPW];
                 int32_t idx8[kCubeRPW];
 #pragma unroll
@@ -1849,9 +1852,11 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
 // wave instruction 1 KiB contiguous whatever P is -- and finally one thread
 // per (i, j) row recomputes the row from LDS for the argmin over k.
 constexpr int kSmallMaxN = 64;
-// default switch-over to the two-rows-per-wave fused kernel: measured per 1000
-// scenes, small vs fused: 48^3 0.219 vs 0.259 ms, 56^3 0.417 vs 0.344 ms
-constexpr int kSmallAutoMaxN = 52;
+// default switch-over to the fused kernel's four-rows-per-wave form: measured
+// per 1000 scenes, small vs fused: 24^3 0.041 vs 0.064 ms, 32^3 0.095 vs
+// 0.072, 40^3 0.138 vs 0.173, 48^3 0.220 vs 0.193, 56^3 0.417 vs 0.261
+// (the fused tiles are 32 j wide: M = 40 leaves 3/8 of them empty)
+constexpr int kSmallAutoMaxN = 44;
 
 struct CubeSmallArgs {
     const double *pts;
@@ -2194,7 +2199,7 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
 //   MVM_PAIRWISE_RPW  rows per wave per group (4 / 8 / 16)
 //   MVM_PAIRWISE_RG   row groups per wave (1..16)
 //   MVM_PAIRWISE_NT   row store policy: 1 nt (default), 0 default, 2 sc1, 3 sc0 sc1
-//   MVM_TRIPLET_SMALL one-workgroup-per-scene cube: unset = views of <= 52, 1 = < 64, 0 = off
+//   MVM_TRIPLET_SMALL one-workgroup-per-scene cube: unset = views of <= 44, 1 = < 64, 0 = off
 //   MVM_TRIPLET_FUSED 1: tiled cube with in-prologue pair residuals (<= 256)
 //   MVM_LSAP_WAVE_MAX_COLS  long-side limit of the one-wave LSAP (mvm_lsap.hip)
 int env_int(const char *name, int dflt) {
@@ -2550,9 +2555,15 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
             return fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                         (long long)blocks);
         const dim3 grid((unsigned)blocks), block(kThreads);
-        // views of <= 128: two rows per wave instruction (MVM_TRIPLET_HALF=0: off)
-        if (tile == 3 && max_n <= kChunk / 2 && env_int("MVM_TRIPLET_HALF", 1)) {
-            triplet_fused_kernel<16, 8, true><<<grid, block, 0, s>>>(c);
+        // views of <= 128 / <= 64: two / four rows per wave instruction
+        // (MVM_TRIPLET_HALF=0: off, 2: at most two)
+        const int split_env = env_int("MVM_TRIPLET_HALF", 1);
+        if (tile == 3 && split_env && max_n <= kChunk / 4 && split_env != 2) {
+            triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
+            return check_launch("triplet_fused_kernel");
+        }
+        if (tile == 3 && split_env && max_n <= kChunk / 2) {
+            triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
             return check_launch("triplet_fused_kernel");
         }
         switch (tile) {

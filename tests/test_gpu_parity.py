@@ -271,7 +271,7 @@ def test_launches_capture_into_a_hip_graph(cuda):
                            r.view(torch.int32) if r.dtype == torch.float32 else r)
 
 
-@pytest.mark.parametrize("n", [520, 100])
+@pytest.mark.parametrize("n", [520, 100, 60])
 def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
     """A row's winning k duplicated in its own lane group, in another lane and
     (views of more than 256) in the same lane of the next 256-chunk and in the

@@ -36,7 +36,8 @@ env = {"tile": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPL
        "generic": {"MVM_TRIPLET_VARIANT": "1"},
        "chunked": {"MVM_TRIPLET_CHUNKED": "1"},
        "nochunk": {"MVM_TRIPLET_CHUNKED": "0"},
-       "nohalf": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_HALF": "0"}}
+       "nohalf": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_HALF": "0"},
+       "split2": {"MVM_TRIPLET_VARIANT": "3", "MVM_TRIPLET_SMALL": "0", "MVM_TRIPLET_FUSED": "1", "MVM_TRIPLET_HALF": "2"}}
 times = {v: [] for v in args.variants.split(",")}
 ref = None
 for rnd in range(args.rounds + 1):
