@@ -5,7 +5,8 @@
  *                v = f32(half(d1 + d2)) with half = exponent decrement (exact
  *                after the f32 cast, tests/test_host_logic.py).
  * Proposal:      the same with every line component multiplied by 0.5 first,
- *                v' = f32(d1' + d2').
+ *                v' = f32(d1' + d2').  Variant B halves the column's line and
+ *                point and only the row line's constant term.
  * Inputs: normalised lines (random angles, some near an axis so one component
  * is tiny or subnormal), l2 and points over many magnitudes within the fast
  * path's tame bounds (|x|,|y| <= 2^40, |l2| <= 2^60), zeros.
@@ -64,7 +65,7 @@ static void line(double l[3]) {
 
 int main(int argc, char **argv) {
     const long long n = argc > 1 ? atoll(argv[1]) : 10000000LL;
-    long long bad = 0;
+    long long bad = 0, badb = 0;
     for (long long i = 0; i < n; ++i) {
         double c[3], r[3];
         line(c);
@@ -78,13 +79,23 @@ int main(int argc, char **argv) {
         const double e1 = fabs(fma(hc[1], ry, hc[0] * rx) + hc[2]);
         const double e2 = fabs(fma(hr[1], cy, hr[0] * cx) + hr[2]);
         const float w = (float)(e1 + e2);
-        uint32_t a, b; memcpy(&a, &v, 4); memcpy(&b, &w, 4);
+        /* variant B: halve the column's line AND point, and the row line's l2 only */
+        const double hcx = 0.5 * cx, hcy = 0.5 * cy, hr2 = 0.5 * r[2];
+        const double g1 = fabs(fma(hc[1], ry, hc[0] * rx) + hc[2]);
+        const double g2 = fabs(fma(r[1], hcy, r[0] * hcx) + hr2);
+        const float wb = (float)(g1 + g2);
+        uint32_t a, b, bb; memcpy(&a, &v, 4); memcpy(&b, &w, 4); memcpy(&bb, &wb, 4);
+        if (a != bb) {
+            if (badb < 8) printf("MISMATCH(B) c=(%a,%a,%a) r=(%a,%a,%a) p=(%a,%a) q=(%a,%a): %a vs %a\n",
+                                 c[0], c[1], c[2], r[0], r[1], r[2], rx, ry, cx, cy, v, wb);
+            ++badb;
+        }
         if (a != b) {
             if (bad < 8) printf("MISMATCH c=(%a,%a,%a) r=(%a,%a,%a) p=(%a,%a) q=(%a,%a): %a vs %a\n",
                                 c[0], c[1], c[2], r[0], r[1], r[2], rx, ry, cx, cy, v, w);
             ++bad;
         }
     }
-    printf("checked %lld pairs, %lld float32 mismatches\n", n, bad);
-    return bad != 0;
+    printf("checked %lld pairs, %lld float32 mismatches (half lines), %lld (variant B: half column, half row l2)\n", n, bad, badb);
+    return bad != 0 || badb != 0;
 }
