@@ -11,10 +11,12 @@ the single gather of every rank's association rows to rank 0 (RCCL/xGMI).
 
 Default workload (``c3``, BASELINE.json configs[2], the configuration the
 @1/2/4/8-GPU metric is quoted on via configs[3]): 4 cameras x 1024
-detections/view x 10,000 scenes PER GPU (weak scaling: each rank owns its own
-10k-scene shard), 6 camera pairs -> 6.29e10 detection pairs per GPU per step.
-Scenes are processed in launches of ``--chunk`` scenes; every residual is
-stored to HBM (a chunk-sized buffer is reused across launches).
+detections/view x 10,000 scenes, 6 camera pairs -> 6.29e10 detection pairs
+per step.  With N GPUs the 10,000 scenes are split over the ranks (strong
+scaling, the default), so ``--gpus 8`` is configs[3]: 1,250 scenes per GPU;
+``--scaling weak`` gives every rank its own 10,000.  Scenes are processed in
+equal launches of at most ``--chunk`` scenes; every residual is stored to HBM
+(a launch-sized buffer is reused across launches).
 
 Printed by rank 0: ONE JSON line with value = total pairs/s over all ranks,
 the dominant kernel's roofline (achieved algorithmic GB/s from HIP events on
@@ -37,7 +39,7 @@ sys.path.insert(0, REPO)
 
 from bpc_baseline_amd import ops  # noqa: E402
 from bpc_baseline_amd.distributed import (ChunkedRowGather, gather_rows, init_from_env,  # noqa: E402
-                                          max_over_ranks)
+                                          max_over_ranks, sum_over_ranks)
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
@@ -195,6 +197,58 @@ def cpu_baseline(batch, mode: str, target_s: float):
                       f"OpenMP x{threads} on {cpu_model()}"}
 
 
+class ClockSampler:
+    """Samples the GPU's current shader clock (the starred level of
+    /sys/class/drm/card*/device/pp_dpm_sclk) on a host thread while the timed
+    region runs, so box-to-box spread can be attributed to clocks or not."""
+
+    def __init__(self, period_s: float = 0.01):
+        import glob
+        import threading
+        self.paths = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+        self.period = period_s
+        self.samples = []
+        self.stop_ev = threading.Event()
+        self.thread = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        vals = []
+        for p in self.paths:
+            try:
+                with open(p) as fh:
+                    for line in fh:
+                        if line.rstrip().endswith("*"):
+                            vals.append(int(line.split(":")[1].strip().split("Mhz")[0].split("MHz")[0]))
+            except (OSError, ValueError, IndexError):
+                pass
+        return max(vals) if vals else None
+
+    def _run(self):
+        while not self.stop_ev.is_set():
+            v = self._read()
+            if v is not None:
+                self.samples.append(v)
+            self.stop_ev.wait(self.period)
+
+    def __enter__(self):
+        if self.paths:
+            self.thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop_ev.set()
+        if self.thread.is_alive():
+            self.thread.join()
+
+    def summary(self):
+        if not self.samples:
+            return {"source": "pp_dpm_sclk unreadable", "samples": 0}
+        s = np.asarray(self.samples, dtype=np.float64)
+        return {"source": "pp_dpm_sclk (starred level, max over visible cards)",
+                "samples": int(s.size), "mean_mhz": float(s.mean()), "min_mhz": float(s.min()),
+                "max_mhz": float(s.max())}
+
+
 def load_traffic(workload: str, scenes_per_launch: int):
     """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json), only if it
     was collected on this workload at this launch size."""
@@ -217,8 +271,13 @@ def main():
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (override)")
     ap.add_argument("--chunk", type=int, default=None, help="scenes per launch (override)")
-    ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
-                    help="weak: --scenes per GPU; strong: --scenes split over the GPUs")
+    ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                    help="strong (default): --scenes split over the GPUs, so --gpus 8 measures "
+                         "BASELINE configs[3] (C3's 10k scenes, 1,250 per GPU); weak: --scenes "
+                         "per GPU")
+    ap.add_argument("--dump-association", default=None, metavar="DIR",
+                    help="rank 0 saves the gathered association rows (argmin.npy, minval.npy, "
+                         "in global scene order) after the timed region")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target length of the CPU-baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
@@ -249,7 +308,10 @@ def main():
     t0 = time.perf_counter()
     batch = make_scenes(n_local, wl["n_cams"], wl["n_dets"], seed=args.seed, first_scene=first)
     log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
-    chunks, n_rows = build_chunks(batch, min(wl["chunk"], n_local), dev, wl["mode"])
+    # equal launches of at most --chunk scenes (1,250 scenes -> 2 x 625, not 1000 + 250)
+    n_launch = max(1, -(-n_local // wl["chunk"]))
+    chunk = -(-n_local // n_launch)
+    chunks, n_rows = build_chunks(batch, chunk, dev, wl["mode"])
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
     max_units = max(c.units for c in chunks)
@@ -320,20 +382,52 @@ def main():
     events = []
     torch.cuda.synchronize(dev)
     env.barrier()
-    t_start = time.perf_counter()
-    if graph is not None:   # one event pair over the timed region: no markers between steps
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ev0.record(stream)
-    for _ in range(args.steps):
-        gathered = step(events)
-    if graph is not None:
-        ev1.record(stream)
-        events.append((ev0, ev1, step_bytes * args.steps, units_local * args.steps,
-                       len(chunks) * args.steps))
-    torch.cuda.synchronize(dev)
-    env.barrier()
-    elapsed = time.perf_counter() - t_start
+    with ClockSampler() as clocks:
+        t_start = time.perf_counter()
+        if graph is not None:   # one event pair over the timed region: no markers between steps
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record(stream)
+        for _ in range(args.steps):
+            gathered = step(events)
+        if graph is not None:
+            ev1.record(stream)
+            events.append((ev0, ev1, step_bytes * args.steps, units_local * args.steps,
+                           len(chunks) * args.steps))
+        torch.cuda.synchronize(dev)
+        env.barrier()
+        elapsed = time.perf_counter() - t_start
     elapsed = max_over_ranks(env, elapsed)
+
+    # ---- N > 1: the step's two parts timed apart (untimed for `value`) -----
+    # compute alone (every launch, no collective) and the association gather
+    # alone, each bracketed by barrier + sync and maxed over ranks
+    split = None
+    if env.initialised:
+        reps = max(1, min(args.steps, 5))
+        torch.cuda.synchronize(dev)
+        env.barrier()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            for c in chunks:
+                launch(c)
+        torch.cuda.synchronize(dev)
+        env.barrier()
+        t_comp = max_over_ranks(env, time.perf_counter() - t0) / reps
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            if overlap:
+                for k in range(len(chunks)):
+                    gatherer.issue(k)
+                gatherer.finish()
+            else:
+                gather_rows(env, argmin, minval)
+        torch.cuda.synchronize(dev)
+        env.barrier()
+        t_gath = max_over_ranks(env, time.perf_counter() - t0) / reps
+        split = {"compute_ms": t_comp * 1e3, "gather_ms": t_gath * 1e3,
+                 "gather_bytes_per_rank": int(n_rows * 8),
+                 "note": "each part alone, barrier + sync around, max over ranks; in the timed "
+                         "step the gather pieces overlap the next launches"}
 
     # ---- kernel roofline from the events (on the launch stream) ------------
     # (with a graph, one event pair brackets a step's launches)
@@ -349,6 +443,14 @@ def main():
     if env.initialised and env.is_root and gathered is not None:
         g_am = gathered[0].reshape(-1)[:n_rows].to(argmin.device)
         gather_check = "rank-0 rows equal after gather" if torch.equal(g_am, argmin) else "MISMATCH"
+    if args.dump_association and env.is_root:
+        os.makedirs(args.dump_association, exist_ok=True)
+        if env.initialised:
+            g_am, g_mv = (g.reshape(-1).cpu().numpy() for g in gathered[:2])
+        else:
+            g_am, g_mv = argmin.cpu().numpy(), minval.cpu().numpy()
+        np.save(os.path.join(args.dump_association, "argmin.npy"), g_am)
+        np.save(os.path.join(args.dump_association, "minval.npy"), g_mv)
 
     # ---- parity spot-check of the last launch (untimed) --------------------
     parity = "skipped"
@@ -422,15 +524,16 @@ def main():
         probe_gbs = 5 * dist_buf.numel() * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
 
 
+    units_all = sum_over_ranks(env, units_local)   # ragged shards differ by one scene
     if not env.is_root:
         return
-    total_units = units_local * world * args.steps
+    total_units = units_all * args.steps
     value = total_units / elapsed
     unit = "pairs/s" if wl["mode"] == "pairwise" else "triples/s"
     cpu = None
     if world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, wl["mode"], args.cpu_seconds)
-    traffic = load_traffic(args.workload, min(wl["chunk"], n_local))
+    traffic = load_traffic(args.workload, chunk)
     out = {
         "metric": METRIC if wl["mode"] == "pairwise" else "cost-cube triples/sec",
         "value": value,
@@ -447,16 +550,24 @@ def main():
         "config": {
             "workload": wl["desc"],
             "n_cams": wl["n_cams"], "n_dets": wl["n_dets"],
-            "n_scenes_per_gpu": n_local if args.scaling == "weak" else None,
+            "n_scenes_per_gpu": n_local,
             "n_scenes_total": n_local * world if args.scaling == "weak" else wl["n_scenes"],
-            "scenes_per_launch": wl["chunk"], "launches_per_step": len(chunks),
+            "scenes_per_launch": chunk, "launches_per_step": len(chunks),
             "units_per_gpu_step": units_local,
             "launch": ("one hipGraph replay per step (captured once, outside the timed region)"
                        if graph is not None else "eager op calls"),
             "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
                             f"({env.backend}{', overlapped per launch' if overlap else ''})")
                            if env.initialised else "single GPU",
+            "baseline_config": ("configs[3]: C3 scene-sharded across the GPUs"
+                                if args.workload == "c3" and args.scaling == "strong" and world > 1
+                                else None),
         },
+        "process_group": ({"world_size": world, "backend": env.backend,
+                           "source": "torch.distributed.get_world_size()/get_backend() after init"}
+                          if env.initialised else None),
+        "step_split": split,
+        "sclk": clocks.summary(),
         "roofline": {
             "bound": "hbm",
             "kernel": ("pairwise_kernel" if wl["mode"] == "pairwise"

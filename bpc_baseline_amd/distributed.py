@@ -19,7 +19,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["DistEnv", "init_from_env", "shard_range", "gather_rows", "max_over_ranks",
-           "ChunkedRowGather"]
+           "sum_over_ranks", "ChunkedRowGather"]
 
 
 class DistEnv:
@@ -67,6 +67,9 @@ def init_from_env(backend: Optional[str] = None, use_gpu: bool = True) -> DistEn
         kw = {"device_id": device} if (use_gpu and backend == "nccl") else {}
         dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
         initialised = True
+        # what the process group itself reports, not what the launcher's env said
+        world, rank = dist.get_world_size(), dist.get_rank()
+        backend = str(dist.get_backend())
     return DistEnv(rank, world, local_rank, device, initialised, backend)
 
 
@@ -109,6 +112,15 @@ def max_over_ranks(env: DistEnv, value: float) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(env: DistEnv, value: int) -> int:
+    if not env.initialised:
+        return int(value)
+    dev = env.device if env.backend == "nccl" else torch.device("cpu")
+    t = torch.tensor([int(value)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return int(t.item())
 
 
 class ChunkedRowGather:

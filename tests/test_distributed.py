@@ -111,6 +111,63 @@ def test_bench_rccl_process_group_single_rank(tmp_path):
     assert "nccl" in line["config"]["parallelism"]
 
 
+def _run_bench(repo, argv, env, tmp_path, name):
+    import subprocess
+    import sys
+    r = subprocess.run(argv, env=env, capture_output=True, text=True, timeout=400, cwd=repo)
+    (tmp_path / f"{name}.err").write_text(r.stderr)
+    assert r.returncode == 0, f"{name}: rc {r.returncode}\n{r.stderr[-3000:]}"
+    import json
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_scenes", [24, 25])
+def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
+    """bench.py under torchrun with 2 ranks sharing the one GPU (gloo group):
+    each rank runs libmvmatch.so's pairwise kernel on its own scene shard, the
+    association rows are gathered to rank 0 (chunked async gathers for equal
+    shards, the one-shot padded gather for 13 + 12 scenes), and rank 0's
+    gathered rows equal a single-process run of the same scenes bit for bit,
+    and the oracle's np.argmin rows (process_pose.py:154-159: scenes are
+    independent, so sharding must not change any row)."""
+    import sys
+    from bpc_baseline_amd.synth import make_scenes
+    from oracle import oracle as O
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    common = ["--workload", "c3", "--scenes", str(n_scenes), "--chunk", "8", "--steps", "1",
+              "--warmup", "1", "--cpu-seconds", "0"]
+    env1 = dict(os.environ)
+    for k in ("MVM_DIST_FORCE", "MVM_DIST_BACKEND", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env1.pop(k, None)
+    single = _run_bench(repo, [sys.executable, "bench.py", *common, "--graph", "off",
+                               "--dump-association", str(tmp_path / "single")],
+                        env1, tmp_path, "single")
+    env2 = dict(env1, MVM_DIST_BACKEND="gloo")
+    multi = _run_bench(repo, [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                              "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                              "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                              *common, "--dump-association", str(tmp_path / "multi")],
+                       env2, tmp_path, "multi")
+    assert multi["n_gpus"] == 2
+    assert multi["process_group"]["world_size"] == 2
+    assert multi["process_group"]["backend"] == "gloo"
+    assert multi["config"]["n_scenes_total"] == n_scenes
+    assert multi["gather_check"] == "rank-0 rows equal after gather"
+    assert multi["parity"].startswith("bit-exact") and single["parity"].startswith("bit-exact")
+    assert multi["step_split"]["gather_ms"] > 0
+    a1 = np.load(tmp_path / "single" / "argmin.npy")
+    m1 = np.load(tmp_path / "single" / "minval.npy")
+    a2 = np.load(tmp_path / "multi" / "argmin.npy")
+    m2 = np.load(tmp_path / "multi" / "minval.npy")
+    assert np.array_equal(a1, a2)
+    assert np.array_equal(m1.view(np.int32), m2.view(np.int32))
+    b = make_scenes(n_scenes, 4, 1024, seed=0)
+    _, ra, rm, _, _ = O.pairwise(b.pts, b.cam_offs, b.F, b.pairs, n_scenes, 4, want_dist=False)
+    assert np.array_equal(a2, ra)
+    assert np.array_equal(m2.view(np.int32), rm.view(np.int32))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("workload", ["c3", "c2cube"])
 def test_bench_graph_replay_single_gpu(tmp_path, workload):
