@@ -13,13 +13,49 @@ import os
 import re
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-# MVM_LIB_PATH: an alternative in-tree build for A/B timing (tools/ only)
+# MVM_LIB_PATH: an alternative in-tree build for A/B timing (tools/ only; the
+# library itself reads no environment)
 LIB_PATH = os.environ.get("MVM_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libmvmatch.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "mvmatch.h")
 
 MVM_OK = 0
 MVM_MAX_CAMS = 8
 MVM_MAX_PAIRS = 28
+MVM_F32, MVM_F64 = 0, 1
+
+# enum values of include/mvmatch.h
+PAIRWISE_ARGMIN = {"default": 0, "lazy_transposed": 1, "lazy_rows": 2, "eager": 3}
+CUBE_KERNEL = {"default": 0, "small": 1, "fused": 2, "workspace": 3, "generic": 4}
+
+
+class MvmOptions(ctypes.Structure):
+    """``mvm_options`` (include/mvmatch.h): kernel-path selection; every field
+    0 = the compiled-in default.  The choices never change results."""
+    _fields_ = [(n, ctypes.c_int32) for n in (
+        "size", "pairwise_argmin", "pairwise_rows_per_wave", "pairwise_row_groups",
+        "cube_kernel", "cube_rows_per_instr", "lsap_wave_max_cols", "lsap_multi_g",
+        "lsap_lds_max_cols", "lsap_lds_small_cols", "lsap_mid_max_cols")]
+
+
+OPTION_FIELDS = [n for n, _ in MvmOptions._fields_[1:]]
+
+
+def make_options(**kw):
+    """MvmOptions from keyword fields (names above; enum fields also accept the
+    names in PAIRWISE_ARGMIN / CUBE_KERNEL).  No keywords -> None (defaults)."""
+    if not kw:
+        return None
+    o = MvmOptions()
+    o.size = ctypes.sizeof(MvmOptions)
+    for k, v in kw.items():
+        if k not in OPTION_FIELDS:
+            raise ValueError(f"unknown mvm_options field {k!r}")
+        if k == "pairwise_argmin" and isinstance(v, str):
+            v = PAIRWISE_ARGMIN[v]
+        if k == "cube_kernel" and isinstance(v, str):
+            v = CUBE_KERNEL[v]
+        setattr(o, k, int(v))
+    return o
 
 
 class MvmError(RuntimeError):
@@ -40,11 +76,17 @@ SIGNATURES = {
     "mvm_version": (ctypes.c_char_p, []),
     "mvm_last_error_string": (ctypes.c_char_p, []),
     "mvm_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "mvm_options_init": (None, [_vp]),
     "mvm_pairwise_residual_argmin": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp,            # pts, cam_offs, F, pair_a (host), pair_b (host)
         _i32, _i32, _i32, _i32,             # n_scenes, n_cams, n_pairs, max_n
         _vp, _vp, _vp, _vp, _vp,            # dist_offs, row_offs, dist, argmin, minval
         _vp]),                              # stream
+    "mvm_pairwise_residual_argmin_ex": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp,
+        _i32, _i32, _i32, _i32,
+        _vp, _vp, _vp, _vp, _vp,
+        _vp, _vp]),                         # options (host), stream
     "mvm_pairwise_residual_f64": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp,
         _i32, _i32, _i32, _i32,
@@ -55,7 +97,12 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
         _vp, _vp, _vp, _vp, _vp,            # cube_offs, row_offs, cube, argmin, minval
         _vp, _sz, _vp]),                    # workspace, workspace_bytes, stream
+    "mvm_triplet_cost_argmin_ex": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _i32,
+        _vp, _vp, _vp, _vp, _vp,
+        _vp, _sz, _vp, _vp]),               # workspace, bytes, options (host), stream
     "mvm_lsap_plan": (_i64, [_i32, _vp, _vp, _vp, _vp]),
+    "mvm_lsap_plan_ex": (_i64, [_i32, _vp, _vp, _i32, _vp, _vp]),
     "mvm_lsap_solve": (ctypes.c_int, [
         _vp, _vp, _vp, _i32, _vp, _vp,      # cost, cost_offs, dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp, _vp]),     # workspace, bytes, row_ind, col_ind, status, stream
@@ -63,6 +110,10 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _vp, _vp,
         _vp, _sz, _vp, _vp, _vp,
         _i64, _i64, _vp]),                  # long_min, long_max, stream
+    "mvm_lsap_solve_ex": (ctypes.c_int, [
+        _vp, _i32, _vp, _vp, _i32, _vp, _vp,   # cost, dtype, cost_offs, dims, n, ws_offs, out_offs
+        _vp, _sz, _vp, _vp, _vp,            # workspace, bytes, row_ind, col_ind, status
+        _i64, _i64, _vp, _vp]),             # long_min, long_max, options (host), stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
         ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id

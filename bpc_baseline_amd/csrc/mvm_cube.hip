@@ -1,0 +1,1228 @@
+// mvm_cube.hip — the three-camera cost cube (compute_cost_matrix) and its C ABI.
+//
+// Reference: bpc/inference/epipolar_matching.py
+//   compute_cost_matrix (:83-98)  cube[i][j][k] = float32(epipolar_error_full)
+//   epipolar_error_full (:73-81)  ((e12 + e13) + e23) / 3 in fp64
+//   (new)          per-(i, j) argmin over k of the stored float32
+//
+// HBM-write bound: 4 bytes per triple out, O(n) in.  Four kernels, picked by
+// the batch's largest view: a one-workgroup-per-scene
+// kernel for IPD-sized views, fused 16 i x 32 j tiles whose pair residuals
+// are computed in the prologue (k-chunked above 256), and a workspace form
+// (fp64 pair matrices, then tiles or one row per wave) kept as the exact
+// generic path.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include <stdint.h>
+
+#include "mvmatch.h"
+#include "mvm_device.h"
+#include "mvm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kTripletRowsPerWave = 8;   // generic kernel: 32 (i, j) rows per workgroup
+
+// --------------------------------------------------------- triplet kernel ----
+struct CubeArgs {
+    const int64_t *cam_offs;    // [S*3 + 1]
+    const double *e;            // fp64 pair matrices (e12, e13, e23 per scene)
+    int64_t mat_stride;         // elements between consecutive matrices
+    int64_t ld;                 // row stride of every matrix (multiple of 4)
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t i_count;            // max_n (grid i extent)
+    int32_t j_blocks;
+};
+
+// ((e12 + e13) + e23) / 3 -> float32  (epipolar_matching.py:78-81, :96)
+__device__ __forceinline__ double triple_cost(double e12, double e13, double e23) {
+    return ((e12 + e13) + e23) / 3.0;
+}
+
+template <int RPW>
+__global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
+    const int t = threadIdx.x;
+    const int wave = t / kWave;
+    const int lane = t % kWave;
+    const int jb = (int)(blockIdx.x % (uint32_t)args.j_blocks);
+    const int si = (int)(blockIdx.x / (uint32_t)args.j_blocks);
+    const int s = si / args.i_count;
+    const int i = si - s * args.i_count;
+    const int64_t o1 = args.cam_offs[3 * (int64_t)s];
+    const int N = (int)(args.cam_offs[3 * (int64_t)s + 1] - o1);
+    const int M = (int)(args.cam_offs[3 * (int64_t)s + 2] - args.cam_offs[3 * (int64_t)s + 1]);
+    const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
+    const int j0 = jb * kWaves * RPW + wave * RPW;
+    if (i >= N || j0 >= M) return;   // uniform over the wave (no barriers below)
+
+    const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
+    const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride + (int64_t)i * args.ld;
+    const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
+    const int64_t coff = args.cube_offs[s];
+    const bool vec_ok = ((coff & 3) == 0) && ((P & 3) == 0);
+
+    uint32_t bkey[RPW];
+    int32_t bidx[RPW];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        bkey[r] = kKeyInvalid;
+        bidx[r] = 0x7FFFFFFF;
+    }
+
+    for (int c0 = 0; c0 < P; c0 += kChunk) {
+        const int kbase = c0 + kColsPerLane * lane;
+        const bool full = vec_ok && (c0 + kChunk <= P);
+        double a13[kColsPerLane];
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) a13[q] = (kbase + q < P) ? e13[kbase + q] : 0.0;
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int j = j0 + r;
+            if (j >= M) break;
+            const double v12 = e12[(int64_t)i * args.ld + j];
+            const double *e23r = e23 + (int64_t)j * args.ld;
+            double e[kColsPerLane];
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                const double v23 = (kbase + q < P) ? e23r[kbase + q] : 0.0;
+                e[q] = triple_cost(v12, a13[q], v23);
+            }
+            float *crow = args.cube ? args.cube + coff + ((int64_t)i * M + j) * P : nullptr;
+            if (crow) {
+                if (full) {
+                    store4_nt(crow + kbase, e);
+                } else {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q)
+                        if (kbase + q < P) crow[kbase + q] = (float)e[q];   // L2 merges strided dwords
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                const uint32_t k = (kbase + q < P) ? key_of((float)e[q]) : kKeyInvalid;
+                if (k < bkey[r]) {
+                    bkey[r] = k;
+                    bidx[r] = kbase + q;
+                }
+            }
+        }
+    }
+
+    const int64_t roff = args.row_offs[s];
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) {
+        const int j = j0 + r;
+        if (j >= M) break;
+        uint32_t kmin;
+        int32_t imin;
+        wave_argmin(bkey[r], bidx[r], kmin, imin);
+        if (lane == 0) {
+            const int64_t row = roff + (int64_t)i * M + j;
+            if (args.argmin) args.argmin[row] = (kmin == kKeyInvalid) ? -1 : imin;
+            if (args.minval) args.minval[row] = value_of_key(kmin);
+        }
+    }
+}
+
+// ------------------------------------------------- fast triplet kernel ----
+constexpr double kThird = 1.0 / 3.0;
+// residual bound under which a sum of three is finite (tile-wide fast path)
+constexpr double kTameResidual = 0x1p1020;
+
+// 4 consecutive doubles at a 16-byte aligned address (two dwordx4 loads);
+// lanes past the view's end read zeros.
+__device__ __forceinline__ void load4(const double *p, int valid, double out[4]) {
+    if (valid >= 4) {
+        const f64x2 lo = *reinterpret_cast<const f64x2 *>(p);
+        const f64x2 hi = *reinterpret_cast<const f64x2 *>(p + 2);
+        out[0] = lo.x;
+        out[1] = lo.y;
+        out[2] = hi.x;
+        out[3] = hi.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[q] = q < valid ? p[q] : 0.0;
+    }
+}
+
+// RN(s / 3) by one Markstein correction (the default): with y = RN(1/3) and
+// q0 = RN(s * y) within one ulp of s/3, r = fma(-q0, 3, s) is exact and
+// q1 = fma(r, y, q0) is the correctly rounded quotient -- for every finite s
+// (checked against the IEEE division on 1.1e9 random, binade-edge,
+// subnormal and near-midpoint inputs, tools/probes/third_markstein.c, and in
+// tests/test_host_logic.py).  Three fp64 ops and a finiteness test instead
+// of a product plus a float32-midpoint/range test (~8 ops, measured 12%
+// slower at 256^3); only non-finite sums (inf: q1 = NaN) take the division.
+// A sum of residuals is never -0, the one input whose sign the correction
+// would not keep.
+__device__ __forceinline__ double third_q(double s) {
+    const double q0 = s * kThird;
+    return __builtin_fma(__builtin_fma(-q0, 3.0, s), kThird, q0);
+}
+
+// true: third_q(s) == RN(s / 3); false: the caller divides
+__device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q); }
+
+// ------------------------------------------- tiled triplet kernel (v3) ----
+// The 3-camera cube for P <= 256 from the fp64 workspace: a workgroup owns
+// (scene, 16 consecutive j, IB consecutive i).  Its prologue loads everything
+// the tile needs -- e23 rows into registers, the e13[i-block][:] and
+// e12[i-block][j-block] tiles into LDS -- with ONE wait; the main loop then
+// issues only LDS reads, VALU work and stores.  This matters on CDNA, where
+// vmcnt counts loads and stores together in issue order: a global load
+// issued after a row store waits for that store's acknowledgement, so loads
+// inside a store-streaming loop stall it.
+
+struct Cube3Args {
+    const int64_t *cam_offs;
+    const double *e;
+    int64_t mat_stride;
+    int64_t ld;
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t j_blocks, i_blocks;
+};
+
+template <int kCubeIB, int kCubeRPW>   // i rows per tile, j rows per wave
+__global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) {
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];              // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kWaves * kCubeRPW];   // 2 KiB
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blockIdx.x / per_scene);
+    const int rem = (int)(blockIdx.x % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t c0 = args.cam_offs[3 * (int64_t)s];
+    const int N = (int)(args.cam_offs[3 * (int64_t)s + 1] - c0);
+    const int M = (int)(args.cam_offs[3 * (int64_t)s + 2] - args.cam_offs[3 * (int64_t)s + 1]);
+    const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
+    const int jw0 = jb * kWaves * kCubeRPW;            // first j of the workgroup
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;              // this wave's first j
+    const int nrows = min(kCubeRPW, M - j0);           // may be <= 0 (scalar)
+
+    const double *e12 = args.e + (int64_t)(3 * s + 0) * args.mat_stride;
+    const double *e13 = args.e + (int64_t)(3 * s + 1) * args.mat_stride;
+    const double *e23 = args.e + (int64_t)(3 * s + 2) * args.mat_stride;
+    const int kb = kColsPerLane * lane;
+    const int kvalid = P - kb;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
+    const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+    const bool act = kvalid > 0;
+
+    // ---- prologue: all loads of the tile, then one barrier ----------------
+    double a23[kCubeRPW][kColsPerLane];
+#pragma unroll
+    for (int r = 0; r < kCubeRPW; ++r)
+        load4(e23 + (int64_t)(j0 + max(0, min(r, nrows - 1))) * args.ld + kb, kvalid, a23[r]);
+    for (int x = t; x < kCubeIB * (kChunk / 2); x += kThreads) {   // e13 tile, 16 B per load
+        const int r = x / (kChunk / 2), c = 2 * (x % (kChunk / 2));
+        f64x2 v = {0.0, 0.0};
+        if (r < ni && c < P) {
+            if (c + 1 < P) {
+                v = *reinterpret_cast<const f64x2 *>(e13 + (int64_t)(i0 + r) * args.ld + c);
+            } else {
+                v.x = e13[(int64_t)(i0 + r) * args.ld + c];
+            }
+        }
+        *reinterpret_cast<f64x2 *>(&s13[r][c]) = v;
+    }
+    for (int x = t; x < kCubeIB * kWaves * kCubeRPW; x += kThreads) {
+        const int r = x / (kWaves * kCubeRPW), c = x % (kWaves * kCubeRPW);
+        s12[r][c] = (r < ni && jw0 + c < M) ? e12[(int64_t)(i0 + r) * args.ld + jw0 + c] : 0.0;
+    }
+    __syncthreads();
+    if (nrows <= 0) return;   // after the barrier: no more barriers below
+
+    for (int ii = 0; ii < ni; ++ii) {
+        const int i = i0 + ii;
+        double a13[kColsPerLane];
+        {
+            const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+            const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+            a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+        }
+        uint32_t key[kCubeRPW];
+        int32_t idx[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            key[r] = kKeyInvalid;
+            idx[r] = 0x7FFFFFFF;
+            if (r >= nrows) continue;   // uniform
+            const double v12 = s12[ii][wave * kCubeRPW + r];
+            double sum[kColsPerLane], q0[kColsPerLane];
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) {
+                sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                q0[q] = third_q(sum[q]);
+                ok &= third_ok(q0[q]);
+            }
+            float v[kColsPerLane];
+            const int64_t row = (int64_t)i * M + j0 + r;
+            if (full && __all(ok || !act)) {
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                if (act) {
+                    store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                  (uint32_t)kb * 4u, v);
+                }
+                Best b{v[0], kb};
+#pragma unroll
+                for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                idx[r] = act ? b.j : 0x7FFFFFFF;
+            } else {
+                Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                // the IEEE division only when some lane needs it (uniform branch)
+                double qq[kColsPerLane];
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                if (!__all(ok || !act)) {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q)
+                        qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                }
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    v[q] = (float)qq[q];
+                    if (q < kvalid) {
+                        if (args.cube)
+                            args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
+                        best_update_safe(b, v[q], kb + q);
+                    }
+                }
+                key[r] = best_key(b);
+                idx[r] = b.j;
+            }
+        }
+        uint32_t kmin[kCubeRPW];
+        int32_t imin[kCubeRPW];
+#pragma unroll
+        for (int r = 0; r < kCubeRPW; ++r) {
+            kmin[r] = kKeyInvalid;
+            imin[r] = 0;
+            if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+        }
+        store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                    roff + (int64_t)i * M + j0);
+    }
+}
+
+// ------------------------------------------- fused tiled cube (v4) ----
+// triplet_tile_kernel without the fp64 workspace: the prologue computes the
+// tile's pair residuals from the centroids and F directly (exactly row_safe's
+// arithmetic) instead of loading them -- e23 for the wave's RPW j rows and the
+// lane's 4 k into registers, e13 [IB][P] and e12 [IB][4*RPW] into LDS -- so
+// the cube costs one launch and no workspace write + read (the
+// workspace was ~10% of the cube's HBM traffic at 256^3).
+struct CubeFusedArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;            // [S*3, 9]: F12, F13, F23
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t j_blocks, i_blocks;
+};
+
+struct LineRec {
+    double l0, l1, l2;
+    double deg;                 // 1.0: degenerate line (9999 sentinel)
+};
+
+__device__ __forceinline__ double pair_e(const LineRec &col, const LineRec &row, double rx,
+                                         double ry, double cx, double cy) {
+    const double d1 = col.deg != 0.0 ? kSentinel : line_dist(col.l0, col.l1, col.l2, rx, ry);
+    const double d2 = row.deg != 0.0 ? kSentinel : line_dist(row.l0, row.l1, row.l2, cx, cy);
+    return 0.5 * (d1 + d2);                                                       // :28
+}
+
+__device__ __forceinline__ void load_f(const double *F, double f[9]) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) f[q] = F[q];
+}
+
+// SPLIT 2 / 4 (views of <= 128 / <= 64 detections, kCubeRPW == 8): the wave
+// splits into SPLIT lane groups of 64/SPLIT lanes, each taking one (i, j) row
+// with lanes along k (4 k per lane), so a wave instruction covers SPLIT rows
+// and no lane idles past P <= 256/SPLIT; a lane computes wave rows
+// r + (8/SPLIT)*(its group).  The argmin of the 8 rows is the transposed
+// butterfly over keys that are invalid outside each row's group.
+template <int kCubeIB, int kCubeRPW, int SPLIT = 1>
+__global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
+    constexpr bool HALF = SPLIT > 1;   // split mapping
+    static_assert(SPLIT == 1 || (kCubeRPW == 8 && (SPLIT == 2 || SPLIT == 4)), "8 rows in 2 or 4 groups");
+    constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
+    constexpr int kLPR = kWave / SPLIT;           // lanes per row
+    constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
+    __shared__ LineRec s_r13[kCubeIB], s_r12[kCubeIB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[kCubeIB][2], s_p1[kJ][2];
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t blk = blockIdx.x;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blk / per_scene);
+    const int rem = (int)(blk % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
+    const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
+    const int jw0 = jb * kJ;
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;
+    const int nrows = min(kCubeRPW, M - j0);
+    const int hl = lane / kLPR;                                      // row group of the lane
+    const int kb = kColsPerLane * (lane % kLPR);
+    const int kvalid = P - kb;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
+    const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+    const bool act_k = kvalid > 0;
+    const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
+    const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
+    const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
+
+    // ---- prologue 1: the tile's view-0 rows and view-1 rows/columns --------
+    if (t < kCubeIB) {
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (t < ni) {
+            double f[9];
+            px = args.pts[2 * (c0 + i0 + t)];
+            py = args.pts[2 * (c0 + i0 + t) + 1];
+            load_f(F13, f);
+            a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F12, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_r13[t] = a;
+        s_r12[t] = b;
+        s_p0[t][0] = px;
+        s_p0[t][1] = py;
+    } else if (t >= kWave && t < kWave + kJ) {
+        const int jj = t - kWave;
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (jw0 + jj < M) {
+            double f[9];
+            px = args.pts[2 * (c1 + jw0 + jj)];
+            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            load_f(F12, f);
+            a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_c12[jj] = a;
+        s_r23[jj] = b;
+        s_p1[jj][0] = px;
+        s_p1[jj][1] = py;
+    }
+    __syncthreads();
+    // ---- prologue 2: the tile's pair residuals (row_safe's arithmetic) -------
+    bool tame_in = true;   // every residual this thread produced is <= kTameResidual
+    {
+        const int k = t;                                   // kThreads == kChunk: one column each
+        if (k < P) {
+            double f[9];
+            load_f(F13, f);
+            const double x = args.pts[2 * (c2 + k)], y = args.pts[2 * (c2 + k) + 1];
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+#pragma unroll 4
+            for (int r = 0; r < kCubeIB; ++r) {
+                const double e = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+                s13[r][k] = e;
+                tame_in &= e <= kTameResidual;
+            }
+        } else {
+            for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
+        }
+    }
+    for (int x = t; x < kCubeIB * kJ; x += kThreads) {
+        const int r = x / kJ, jj = x % kJ;
+        const double e = (r < ni && jw0 + jj < M)
+                             ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                             : 0.0;
+        s12[r][jj] = e;
+        tame_in &= e <= kTameResidual;
+    }
+    double a23[kLaneRows][kColsPerLane];
+    {
+        double f[9];
+        load_f(F23, f);
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) {
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            double x = 0.0, y = 0.0;
+            if (q < kvalid) {
+                x = args.pts[2 * (c2 + kb + q)];
+                y = args.pts[2 * (c2 + kb + q) + 1];
+                cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < kLaneRows; ++r) {
+                const int rr = r + hl * kLaneRows;            // the wave row
+                const int jj = wave * kCubeRPW + rr;
+                a23[r][q] = (rr < nrows && q < kvalid)
+                                ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
+                                : 0.0;
+                tame_in &= a23[r][q] <= kTameResidual;
+            }
+        }
+    }
+    // every sum of the tile is finite when its three residuals are <= 2^1020
+    // (NaN fails the compare): then third_q is RN(s/3) for all of them and the
+    // main loop needs no per-row check (a loop without the fallback path)
+    const bool tile_fast = __syncthreads_and(tame_in) != 0 && full;
+    if (nrows <= 0) return;   // after the barrier: no more barriers below
+
+    auto main_loop = [&](auto fast_tag) {
+        constexpr bool FAST = decltype(fast_tag)::value;
+        for (int ii = 0; ii < ni; ++ii) {
+            const int i = i0 + ii;
+            double a13[kColsPerLane];
+            {
+                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+            }
+            uint32_t key[kLaneRows];
+            int32_t idx[kLaneRows];
+#pragma unroll
+            for (int r = 0; r < kLaneRows; ++r) {
+                key[r] = kKeyInvalid;
+                idx[r] = 0x7FFFFFFF;
+                if (r >= nrows) continue;   // uniform (the lower half's row is the smaller)
+                const int rr = r + hl * kLaneRows;                 // the wave row
+                const bool act = act_k && rr < nrows;              // HALF: the upper row may not exist
+                const double v12 = s12[ii][wave * kCubeRPW + rr];
+                double sum[kColsPerLane], q0[kColsPerLane];
+                bool ok = true;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                    q0[q] = third_q(sum[q]);
+                    if (!FAST) ok &= third_ok(q0[q]);
+                }
+                float v[kColsPerLane];
+                const int64_t row = (int64_t)i * M + j0 + rr;
+                if (FAST || (full && __all(ok || !act))) {
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                    if (act) {
+                        store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                      (uint32_t)kb * 4u, v);
+                    }
+                    Best b{v[0], kb};
+#pragma unroll
+                    for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                    key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                    idx[r] = act ? b.j : 0x7FFFFFFF;
+                } else {
+                    Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                    // the IEEE division only when some lane needs it (uniform branch)
+                    double qq[kColsPerLane];
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                    if (!__all(ok || !act)) {
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q)
+                            qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                    }
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) {
+                        v[q] = (float)qq[q];
+                        if (act && q < kvalid) {
+                            if (args.cube)
+                                args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
+                            best_update_safe(b, v[q], kb + q);
+                        }
+                    }
+                    key[r] = best_key(b);
+                    idx[r] = b.j;
+                }
+            }
+            if constexpr (HALF) {   // SPLIT rows share a wave: keys of the other groups are invalid
+                uint32_t key8[kCubeRPW];
+                int32_t idx8[kCubeRPW];
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    const bool mine = (r / kLaneRows) == hl;
+                    key8[r] = mine ? key[r % kLaneRows] : kKeyInvalid;
+                    idx8[r] = mine ? idx[r % kLaneRows] : 0x7FFFFFFF;
+                }
+                uint32_t mk;
+                int32_t mi;
+                wave_argmin8_transposed(key8, idx8, lane, mk, mi);
+                if (lane < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                    if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
+                    if (args.minval) args.minval[row] = value_of_key(mk);
+                }
+            } else if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
+                uint32_t mk;
+                int32_t mi;
+                wave_argmin8_transposed(key, idx, lane, mk, mi);
+                if (lane < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                    if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
+                    if (args.minval) args.minval[row] = value_of_key(mk);
+                }
+            } else {
+                uint32_t kmin[kCubeRPW];
+                int32_t imin[kCubeRPW];
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    kmin[r] = kKeyInvalid;
+                    imin[r] = 0;
+                    if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
+                }
+                store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                            roff + (int64_t)i * M + j0);
+            }
+        }
+    };
+    if (tile_fast) main_loop(std::integral_constant<bool, true>{});
+    else main_loop(std::integral_constant<bool, false>{});
+}
+
+// ------------------------------------ fused tiled cube, any P (v5) ----
+// triplet_fused_kernel for views of more than 256 detections: the k axis is
+// walked in chunks of 256.  Per chunk the prologue computes that chunk's
+// e13 [IB][256] (LDS) and the wave's e23 [RPW j][4 k] (registers) exactly as
+// the single-chunk kernel does; the tile's view-0 / view-1 lines and e12 are
+// computed once.  Each (i, j) row's argmin runs across chunks in two lane-
+// distributed registers (row x = ii*RPW + r lives in lane x % 64, slot x / 64):
+// a chunk's wave minimum replaces the running one only if strictly smaller,
+// so the earliest chunk wins ties (np.argmin's first index).
+template <int kCubeIB, int kCubeRPW>
+__global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(CubeFusedArgs args) {
+    constexpr int kJ = kWaves * kCubeRPW;
+    constexpr int kRows = kCubeIB * kCubeRPW;                                      // (i, j) rows per wave
+    constexpr int kSlots = (kRows + kWave - 1) / kWave;
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
+    __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
+    __shared__ LineRec s_r13[kCubeIB], s_r12[kCubeIB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[kCubeIB][2], s_p1[kJ][2];
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    const uint32_t blk = blockIdx.x;
+    const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
+    const int s = (int)(blk / per_scene);
+    const int rem = (int)(blk % per_scene);
+    const int jb = rem % args.j_blocks;
+    const int ib = rem / args.j_blocks;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
+    const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
+    const int jw0 = jb * kJ;
+    const int i0 = ib * kCubeIB;
+    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    const int ni = min(kCubeIB, N - i0);
+    const int j0 = jw0 + wave * kCubeRPW;
+    const int nrows = min(kCubeRPW, M - j0);
+    const int kb = kColsPerLane * lane;
+    const int64_t coff = args.cube_offs[s];
+    const int64_t roff = args.row_offs[s];
+    const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
+    const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
+    const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
+
+    // ---- once per tile: view-0 rows, view-1 rows/columns, e12 ---------------
+    if (t < kCubeIB) {
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (t < ni) {
+            double f[9];
+            px = args.pts[2 * (c0 + i0 + t)];
+            py = args.pts[2 * (c0 + i0 + t) + 1];
+            load_f(F13, f);
+            a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F12, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_r13[t] = a;
+        s_r12[t] = b;
+        s_p0[t][0] = px;
+        s_p0[t][1] = py;
+    } else if (t >= kWave && t < kWave + kJ) {
+        const int jj = t - kWave;
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (jw0 + jj < M) {
+            double f[9];
+            px = args.pts[2 * (c1 + jw0 + jj)];
+            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            load_f(F12, f);
+            a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_c12[jj] = a;
+        s_r23[jj] = b;
+        s_p1[jj][0] = px;
+        s_p1[jj][1] = py;
+    }
+    __syncthreads();
+    bool tame12 = true;   // as triplet_fused_kernel's tame_in, for this thread's e12
+    for (int x = t; x < kCubeIB * kJ; x += kThreads) {
+        const int r = x / kJ, jj = x % kJ;
+        const double e = (r < ni && jw0 + jj < M)
+                             ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                             : 0.0;
+        s12[r][jj] = e;
+        tame12 &= e <= kTameResidual;
+    }
+    uint32_t run_k[kSlots];
+    int32_t run_i[kSlots];
+#pragma unroll
+    for (int z = 0; z < kSlots; ++z) {
+        run_k[z] = kKeyInvalid;
+        run_i[z] = 0;
+    }
+
+    for (int kc = 0; kc < P; kc += kChunk) {
+        const int Pc = min(kChunk, P - kc);
+        const int kvalid = Pc - kb;
+        if (kc > 0) __syncthreads();   // every wave is done with the previous chunk's s13
+        bool tame_in = tame12;
+        {   // e13 of this chunk: one column per thread
+            const int k = t;
+            double f13[9];
+            load_f(F13, f13);
+            if (k < Pc) {
+                const double x = args.pts[2 * (c2 + kc + k)], y = args.pts[2 * (c2 + kc + k) + 1];
+                LineRec cl{0.0, 0.0, 0.0, 0.0};
+                cl.deg = col_line(f13, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+#pragma unroll 4
+                for (int r = 0; r < kCubeIB; ++r) {
+                    const double e = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
+                    s13[r][k] = e;
+                    tame_in &= e <= kTameResidual;
+                }
+            } else {
+                for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
+            }
+        }
+        double a23[kCubeRPW][kColsPerLane];
+        double f23[9];
+        load_f(F23, f23);
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) {
+            LineRec cl{0.0, 0.0, 0.0, 0.0};
+            double x = 0.0, y = 0.0;
+            if (q < kvalid) {
+                x = args.pts[2 * (c2 + kc + kb + q)];
+                y = args.pts[2 * (c2 + kc + kb + q) + 1];
+                cl.deg = col_line(f23, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
+            }
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                const int jj = wave * kCubeRPW + r;
+                a23[r][q] = (r < nrows && q < kvalid)
+                                ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
+                                : 0.0;
+                tame_in &= a23[r][q] <= kTameResidual;
+            }
+        }
+        const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+        // every sum of this chunk finite: the loop without the per-row vote
+        const bool chunk_fast = __syncthreads_and(tame_in) != 0 && full;
+        if (nrows <= 0) continue;   // uniform; the barriers above are still reached
+
+        const bool act = kvalid > 0;
+        auto chunk_loop = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            for (int ii = 0; ii < ni; ++ii) {
+                const int i = i0 + ii;
+                double a13[kColsPerLane];
+                {
+                    const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                    const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                    a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+                }
+                uint32_t key[kCubeRPW];
+                int32_t idx[kCubeRPW];
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    key[r] = kKeyInvalid;
+                    idx[r] = 0x7FFFFFFF;
+                    if (r >= nrows) continue;   // uniform
+                    const double v12 = s12[ii][wave * kCubeRPW + r];
+                    double sum[kColsPerLane], q0[kColsPerLane];
+                    bool ok = true;
+#pragma unroll
+                    for (int q = 0; q < kColsPerLane; ++q) {
+                        sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
+                        q0[q] = third_q(sum[q]);
+                        if (!FAST) ok &= third_ok(q0[q]);
+                    }
+                    float v[kColsPerLane];
+                    const int64_t row = (int64_t)i * M + j0 + r;
+                    if (FAST || (full && __all(ok || !act))) {
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                        if (act) {
+                            store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
+                                          (uint32_t)kb * 4u, v);
+                        }
+                        Best b{v[0], kb};
+#pragma unroll
+                        for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                        key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
+                        idx[r] = act ? b.j : 0x7FFFFFFF;
+                    } else {
+                        Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+                        // the IEEE division only when some lane needs it (uniform branch)
+                        double qq[kColsPerLane];
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                        if (!__all(ok || !act)) {
+#pragma unroll
+                            for (int q = 0; q < kColsPerLane; ++q)
+                                qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
+                        }
+#pragma unroll
+                        for (int q = 0; q < kColsPerLane; ++q) {
+                            v[q] = (float)qq[q];
+                            if (q < kvalid) {
+                                if (args.cube)
+                                    args.cube[coff + row * P + kc + kb + q] = v[q];
+                                best_update_safe(b, v[q], kb + q);
+                            }
+                        }
+                        key[r] = best_key(b);
+                        idx[r] = b.j;
+                    }
+                }
+                if constexpr (FAST && kCubeRPW == 8 && kWave % 8 == 0) {
+                    // rows x = ii*8 + r land in lanes x % 64 of slot x / 64 directly
+                    const int x0 = ii * kCubeRPW;   // uniform
+                    uint32_t km;
+                    int32_t im;
+                    wave_argmin8_transposed(key, idx, lane, km, im, x0 % kWave);
+                    const bool mine = lane - x0 % kWave >= 0 && lane - x0 % kWave < nrows;
+#pragma unroll
+                    for (int z = 0; z < kSlots; ++z) {
+                        if (z != x0 / kWave) continue;   // uniform
+                        const bool take = mine && km < run_k[z];
+                        run_k[z] = take ? km : run_k[z];
+                        run_i[z] = take ? kc + im : run_i[z];
+                    }
+                    continue;
+                }
+#pragma unroll
+                for (int r = 0; r < kCubeRPW; ++r) {
+                    if (r >= nrows) continue;
+                    uint32_t km;
+                    int32_t im;
+                    wave_argmin(key[r], idx[r], km, im);
+                    const int x = ii * kCubeRPW + r;   // uniform
+                    const bool mine = lane == (x % kWave);
+#pragma unroll
+                    for (int z = 0; z < kSlots; ++z) {
+                        if (z != x / kWave) continue;   // uniform
+                        const bool take = mine && km < run_k[z];
+                        run_k[z] = take ? km : run_k[z];
+                        run_i[z] = take ? kc + im : run_i[z];
+                    }
+                }
+            }
+        };
+        if (chunk_fast) chunk_loop(std::integral_constant<bool, true>{});
+        else chunk_loop(std::integral_constant<bool, false>{});
+    }
+    if (nrows <= 0) return;
+#pragma unroll
+    for (int z = 0; z < kSlots; ++z) {
+        const int x = z * kWave + lane;
+        const int ii = x / kCubeRPW, r = x % kCubeRPW;
+        if (x < kRows && ii < ni && r < nrows) {
+            const int64_t row = roff + (int64_t)(i0 + ii) * M + j0 + r;
+            if (args.argmin) args.argmin[row] = (run_k[z] == kKeyInvalid) ? -1 : run_i[z];
+            if (args.minval) args.minval[row] = value_of_key(run_k[z]);
+        }
+    }
+}
+
+// ------------------------------------------------- small-scene cube ----
+// Scenes whose views hold at most kSmallMaxN detections (the IPD regime: a
+// few to a few dozen objects per image) are too small for the tiled kernel's
+// 16 x 32 tiles and its fp64 workspace pass.  A workgroup owns (scene, block
+// of `ib` rows i): it stages the three views' centroids, the six line sets,
+// e23 [M][P] and its rows of e12 [ib][M], e13 [ib][P] in LDS (exactly the
+// residuals of row_safe: sentinel, 0.5 * (d1 + d2)), then streams its
+// contiguous slice of the cube in flattened order -- 16-byte nontemporal
+// stores, indices advanced incrementally (no divisions in the loop), every
+// wave instruction 1 KiB contiguous whatever P is -- and finally one thread
+// per (i, j) row recomputes the row from LDS for the argmin over k.
+constexpr int kSmallMaxN = 64;
+// default switch-over to the fused kernel's four-rows-per-wave form: measured
+// per 1000 scenes, small vs fused: 24^3 0.041 vs 0.064 ms, 32^3 0.095 vs
+// 0.072, 40^3 0.138 vs 0.173, 48^3 0.220 vs 0.193, 56^3 0.417 vs 0.261
+// (the fused tiles are 32 j wide: M = 40 leaves 3/8 of them empty)
+constexpr int kSmallAutoMaxN = 44;
+
+struct CubeSmallArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;            // [S*3, 9]: F12, F13, F23
+    const int64_t *cube_offs;
+    const int64_t *row_offs;
+    float *cube;
+    int32_t *argmin;
+    float *minval;
+    int32_t max_n;
+    int32_t ib;                 // rows i per workgroup
+    int32_t i_blocks;           // ceil(max_n / ib)
+};
+
+__host__ __device__ inline size_t small_lds_bytes(int nmax, int ib) {
+    return ((size_t)24 * nmax + 2 * (size_t)ib * nmax + (size_t)nmax * nmax) * sizeof(double) +
+           6 * (size_t)nmax;
+}
+
+__device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
+    const double sum = (e12 + e13) + e23;
+    double q = third_q(sum);
+    if (!third_ok(q)) {   // non-finite sum: the IEEE division, skipped when no lane needs it
+        double s2 = sum;
+        __asm__ volatile("" : "+v"(s2));   // keeps the division inside the branch (no if-conversion)
+        q = s2 / 3.0;
+    }
+    return (float)q;
+}
+
+__global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int nmax = args.max_n, IB = args.ib;
+    double *sp = reinterpret_cast<double *>(s_dyn);         // [3][nmax][2] centroids
+    double *sl = sp + 6 * nmax;                              // [3 pairs][2 sides][nmax][3] lines
+    double *s12 = sl + 18 * nmax;                            // [ib][M]
+    double *s13 = s12 + IB * nmax;                           // [ib][P]
+    double *s23 = s13 + IB * nmax;                           // [M][P]
+    unsigned char *sdeg = reinterpret_cast<unsigned char *>(s23 + nmax * nmax);  // [3][2][nmax]
+
+    const int s = blockIdx.x / args.i_blocks, t = threadIdx.x;
+    const int i0 = (blockIdx.x - s * args.i_blocks) * IB;
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t o0 = co[0];
+    const int n[3] = {(int)(co[1] - co[0]), (int)(co[2] - co[1]), (int)(co[3] - co[2])};
+    const int N = n[0], M = n[1], P = n[2];
+    if (i0 >= N || M == 0) return;                           // no (i, j) rows in this block
+    const int nb = min(IB, N - i0);
+    const int64_t roff = args.row_offs[s];
+
+    for (int v = 0; v < 3; ++v) {
+        const int64_t ov = co[v] - o0;
+        for (int q = t; q < 2 * n[v]; q += kThreads) sp[(v * nmax) * 2 + q] = args.pts[2 * (o0 + ov) + q];
+    }
+    __syncthreads();
+    // pair p = (a, b): row lines of view a with F_p, column lines of view b
+    const int pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
+    for (int w = t; w < 6 * nmax; w += kThreads) {
+        const int p = w / (2 * nmax), side = (w / nmax) & 1, i = w % nmax;
+        const int v = side ? pb[p] : pa[p];
+        if (i >= n[v]) continue;
+        double f[9];
+#pragma unroll
+        for (int q = 0; q < 9; ++q) f[q] = args.F[(3 * (int64_t)s + p) * 9 + q];
+        const double x = sp[(v * nmax + i) * 2], y = sp[(v * nmax + i) * 2 + 1];
+        double l0, l1, l2;
+        const bool deg = side ? col_line(f, x, y, l0, l1, l2) : row_line(f, x, y, l0, l1, l2);
+        double *L = sl + ((p * 2 + side) * nmax + i) * 3;
+        L[0] = l0;
+        L[1] = l1;
+        L[2] = l2;
+        sdeg[(p * 2 + side) * nmax + i] = deg;
+    }
+    __syncthreads();
+    // e_ab(i, j) of row_safe: pairs (0,1) and (0,2) for this block's rows, (1,2) whole
+    const int rows_of[3] = {nb, nb, M}, first_of[3] = {i0, i0, 0};
+    double *dst_of[3] = {s12, s13, s23};
+    for (int p = 0; p < 3; ++p) {
+        const int na = rows_of[p], nbb = n[pb[p]], r0 = first_of[p];
+        double *E = dst_of[p];
+        for (int w = t; w < na * nbb; w += kThreads) {
+            const int il = w / nbb, j = w - il * nbb, i = r0 + il;
+            const double *R = sl + ((p * 2 + 0) * nmax + i) * 3;
+            const double *C = sl + ((p * 2 + 1) * nmax + j) * 3;
+            const double rx = sp[(pa[p] * nmax + i) * 2], ry = sp[(pa[p] * nmax + i) * 2 + 1];
+            const double cx = sp[(pb[p] * nmax + j) * 2], cy = sp[(pb[p] * nmax + j) * 2 + 1];
+            const double d1 = sdeg[(p * 2 + 1) * nmax + j] ? kSentinel : line_dist(C[0], C[1], C[2], rx, ry);
+            const double d2 = sdeg[(p * 2 + 0) * nmax + i] ? kSentinel : line_dist(R[0], R[1], R[2], cx, cy);
+            E[w] = 0.5 * (d1 + d2);                                                   // :28
+        }
+    }
+    __syncthreads();
+
+    if (args.cube && P > 0) {
+        const int MP = M * P, total = nb * MP;
+        const int64_t gbase = args.cube_offs[s] + (int64_t)i0 * MP;
+        float *cb = args.cube + gbase;
+        const int head = min(total, (int)((4 - (gbase & 3)) & 3));   // to a 16-byte boundary
+        const int body = (total - head) / 4;                          // float4 groups
+        if (t < head) {
+            const int il = t / MP, r = t - il * MP, j = r / P, k = r - j * P;
+            __builtin_nontemporal_store(cube_f32(s12[il * M + j], s13[il * P + k], s23[j * P + k]), cb + t);
+        }
+        const int tail0 = head + 4 * body;
+        if (t < total - tail0) {
+            const int f = tail0 + t;
+            const int il = f / MP, r = f - il * MP, j = r / P, k = r - j * P;
+            __builtin_nontemporal_store(cube_f32(s12[il * M + j], s13[il * P + k], s23[j * P + k]), cb + f);
+        }
+        if (t < body) {
+            // element f = head + 4g for group g = t + 256 * iter; advance by 1024 elements
+            int f = head + 4 * t;
+            int il = f / MP, r = f - il * MP, j = r / P, k = r - j * P;
+            constexpr int kStep = 4 * kThreads;
+            const int dk = kStep % P, q = kStep / P, dj = q % M, dil = q / M;
+            for (int g = t; g < body; g += kThreads) {
+                float v4[4];
+                int a = il, b = j, c = k;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    v4[e] = cube_f32(s12[a * M + b], s13[a * P + c], s23[b * P + c]);
+                    if (++c == P) {
+                        c = 0;
+                        if (++b == M) {
+                            b = 0;
+                            ++a;
+                        }
+                    }
+                }
+                const f32x4 vv = {v4[0], v4[1], v4[2], v4[3]};
+                __builtin_nontemporal_store(vv, reinterpret_cast<f32x4 *>(cb + head) + g);
+                k += dk;
+                const int ck = k >= P;
+                k -= ck ? P : 0;
+                j += dj + ck;
+                const int cj = j >= M;
+                j -= cj ? M : 0;
+                il += dil + cj;
+            }
+        }
+    }
+    for (int w = t; w < nb * M; w += kThreads) {
+        const int il = w / M, j = w - il * M;
+        uint32_t bk = kKeyInvalid;
+        int32_t bi = -1;
+        const double a = s12[w];
+        for (int k = 0; k < P; ++k) {
+            const uint32_t key = key_of(cube_f32(a, s13[il * P + k], s23[j * P + k]));
+            if (key < bk) {
+                bk = key;
+                bi = k;
+            }
+        }
+        const int64_t row = roff + (int64_t)i0 * M + w;
+        if (args.argmin) args.argmin[row] = bi;
+        if (args.minval) args.minval[row] = value_of_key(bk);
+    }
+}
+
+int grid_check(int64_t blocks) {
+    if (blocks > 0x7FFFFFFFLL)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+    return MVM_OK;
+}
+
+CubeFusedArgs fused_args(const double *pts, const int64_t *cam_offs, const double *F,
+                         const int64_t *cube_offs, const int64_t *row_offs, float *cube,
+                         int32_t *argmin, float *minval, int max_n, int ib) {
+    CubeFusedArgs c{};
+    c.pts = pts;
+    c.cam_offs = cam_offs;
+    c.F = F;
+    c.cube_offs = cube_offs;
+    c.row_offs = row_offs;
+    c.cube = cube;
+    c.argmin = argmin;
+    c.minval = minval;
+    c.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+    c.i_blocks = (max_n + ib - 1) / ib;
+    return c;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+size_t mvm_triplet_workspace_bytes(int32_t n_scenes, int32_t max_n) {
+    if (n_scenes <= 0 || max_n <= 0) return 0;
+    const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;
+    return (size_t)n_scenes * 3 * (size_t)max_n * (size_t)ld * sizeof(double);
+}
+
+int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
+                               const double *F_dev, int32_t n_scenes, int32_t max_n,
+                               const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                               float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                               void *workspace_dev, size_t workspace_bytes,
+                               const mvm_options *opts, mvm_stream_t stream) {
+    mvm_clear_error();
+    mvm_options o;
+    int st = mvm_resolve_options(opts, o);
+    if (st) return st;
+    if (n_scenes < 0 || max_n < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative sizes");
+    if (o.cube_kernel < MVM_CUBE_DEFAULT || o.cube_kernel > MVM_CUBE_GENERIC)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_kernel %d", (int)o.cube_kernel);
+    if (o.cube_rows_per_instr != 0 && o.cube_rows_per_instr != 1 && o.cube_rows_per_instr != 2 &&
+        o.cube_rows_per_instr != 4)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_rows_per_instr %d not 0, 1, 2 or 4",
+                        (int)o.cube_rows_per_instr);
+    if (n_scenes == 0 || max_n == 0) return MVM_OK;
+    if (!pts_dev || !cam_offs_dev || !F_dev || !row_offs_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (cube_dev && !cube_offs_dev) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube without cube_offs");
+    const size_t need = mvm_triplet_workspace_bytes(n_scenes, max_n);
+    if (!workspace_dev || workspace_bytes < need)
+        return mvm_fail(MVM_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
+    if (((uintptr_t)workspace_dev & 15) != 0)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "workspace not 16-byte aligned");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int kernel = o.cube_kernel;
+
+    // the one-workgroup-per-scene kernel: by default up to kSmallAutoMaxN
+    // (measured crossover vs the fused four-rows-per-wave form), on request
+    // up to its limit; everything in LDS, no workspace pass
+    const bool small = kernel == MVM_CUBE_DEFAULT ? max_n <= kSmallAutoMaxN
+                                                  : (kernel == MVM_CUBE_SMALL && max_n < kSmallMaxN);
+    if (small) {
+        CubeSmallArgs c{};
+        c.pts = pts_dev;
+        c.cam_offs = cam_offs_dev;
+        c.F = F_dev;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.max_n = max_n;
+        // rows i per workgroup: the whole scene up to 32 detections, then
+        // 16-row blocks (tools/gpu_cube_small.sh)
+        c.ib = max_n <= 32 ? max_n : 16;
+        c.i_blocks = (max_n + c.ib - 1) / c.ib;
+        const size_t lds = small_lds_bytes(max_n, c.ib);
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute(reinterpret_cast<const void *>(&triplet_small_kernel),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+        const int64_t blocks = (int64_t)n_scenes * c.i_blocks;
+        if ((st = grid_check(blocks))) return st;
+        triplet_small_kernel<<<dim3((unsigned)blocks), dim3(kThreads), lds, s>>>(c);
+        return mvm_check_launch("triplet_small_kernel");
+    }
+    if (kernel == MVM_CUBE_DEFAULT || kernel == MVM_CUBE_SMALL || kernel == MVM_CUBE_FUSED) {
+        const CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
+                                           cube_dev, argmin_dev, minval_dev, max_n, 16);
+        const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
+        if ((st = grid_check(blocks))) return st;
+        const dim3 grid((unsigned)blocks), block(kThreads);
+        if (max_n > kChunk) {
+            // views of more than 256: fused tiles walking k in chunks of 256
+            triplet_fused_chunked_kernel<16, 8><<<grid, block, 0, s>>>(c);
+            return mvm_check_launch("triplet_fused_chunked_kernel");
+        }
+        // tiles of 16 i x 32 j; views of <= 64 / <= 128 put four / two (i, j)
+        // rows in every wave instruction
+        const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
+        if (want >= 4 && max_n <= kChunk / 4)
+            triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
+        else if (want >= 2 && max_n <= kChunk / 2)
+            triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
+        else
+            triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c);
+        return mvm_check_launch("triplet_fused_kernel");
+    }
+    // workspace forms: the fp64 pair matrices e12, e13, e23 of every scene
+    // (pairs (0,1), (0,2), (1,2): F12, F13, F23, process_pose.py:157-159)
+    const int64_t ld = ((int64_t)max_n + 3) / 4 * 4;
+    const int64_t mat_stride = (int64_t)max_n * ld;
+    const int32_t pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
+    st = mvm_pairwise_residual_f64(pts_dev, cam_offs_dev, F_dev, pa, pb, n_scenes, 3, 3, max_n,
+                                   mat_stride, ld, (double *)workspace_dev, stream);
+    if (st) return st;
+    if (kernel == MVM_CUBE_WORKSPACE && max_n <= kChunk) {
+        Cube3Args c{};
+        c.cam_offs = cam_offs_dev;
+        c.e = (const double *)workspace_dev;
+        c.mat_stride = mat_stride;
+        c.ld = ld;
+        c.cube_offs = cube_offs_dev;
+        c.row_offs = row_offs_dev;
+        c.cube = cube_dev;
+        c.argmin = argmin_dev;
+        c.minval = minval_dev;
+        c.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+        c.i_blocks = (max_n + 16 - 1) / 16;
+        const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
+        if ((st = grid_check(blocks))) return st;
+        triplet_tile_kernel<16, 8><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+        return mvm_check_launch("triplet_tile_kernel");
+    }
+    CubeArgs c{};
+    c.cam_offs = cam_offs_dev;
+    c.e = (const double *)workspace_dev;
+    c.mat_stride = mat_stride;
+    c.ld = ld;
+    c.cube_offs = cube_offs_dev;
+    c.row_offs = row_offs_dev;
+    c.cube = cube_dev;
+    c.argmin = argmin_dev;
+    c.minval = minval_dev;
+    c.i_count = max_n;
+    const int rows_per_wg = kWaves * kTripletRowsPerWave;
+    c.j_blocks = (max_n + rows_per_wg - 1) / rows_per_wg;
+    const int64_t blocks = (int64_t)n_scenes * max_n * c.j_blocks;
+    if ((st = grid_check(blocks))) return st;
+    triplet_kernel<kTripletRowsPerWave><<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(c);
+    return mvm_check_launch("triplet_kernel");
+}
+
+int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
+                            const double *F_dev, int32_t n_scenes, int32_t max_n,
+                            const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                            float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                            void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream) {
+    return mvm_triplet_cost_argmin_ex(pts_dev, cam_offs_dev, F_dev, n_scenes, max_n, cube_offs_dev,
+                                      row_offs_dev, cube_dev, argmin_dev, minval_dev, workspace_dev,
+                                      workspace_bytes, nullptr, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,807 @@
+// mvm_pairwise.hip — the pairwise residual kernel (C2/C3 hot path) and its C ABI.
+//
+// Hot path of the reference: bpc/inference/epipolar_matching.py
+//   epipolar_error (:5-28)  ->  pair residual, factorised into per-detection
+//                              normalised epipolar lines (O(n)) + an 8-flop
+//                              fp64 point-line evaluation per pair (O(n^2))
+//   (new) per-row argmin over the stored float32 values
+//
+// Workload shape: HBM-write bound (4 bytes of float32 output per pair, inputs
+// O(n)).  Layout per workgroup (256 threads = 4 waves of 64):
+//   * the workgroup owns 4*RPW*RG rows of one (scene, pair); wave w owns RPW
+//     rows of each of the RG row groups;
+//   * the normalised lines of the view's columns are computed once per
+//     workgroup into LDS; per 256-column chunk every lane of every wave holds
+//     4 consecutive columns in registers and sweeps its RPW rows, so each row
+//     store is one 16-byte-per-lane, 1 KiB-per-wave coalesced store;
+//   * the per-row argmin is tracked per lane in registers across chunks and
+//     reduced across the wave once per row group at the end.
+#include <hip/hip_runtime.h>
+
+#include <stdint.h>
+
+#include "mvmatch.h"
+#include "mvm_device.h"
+#include "mvm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+// ------------------------------------------------------- pairwise kernel ----
+struct PairArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;
+    const int64_t *dist_offs;   // null -> (s*P + p) * mat_stride
+    const int64_t *row_offs;    // null -> no argmin output
+    void *dist;                 // float* or double*; null -> not written
+    int32_t *argmin;
+    float *minval;
+    int64_t mat_stride;
+    int64_t ld;                 // row stride of each matrix; 0 -> n_b
+    int32_t n_cams, n_pairs, row_blocks;
+    int32_t rows_per_wg;        // kWaves * RPW * row groups
+    int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
+    int32_t lazy;               // clean row groups: 2 lazy argmin + transposed reduction,
+                                // 1 lazy + per-row reductions, 0 eager (mvm_options)
+    int32_t pair_a[MVM_MAX_PAIRS];
+    int32_t pair_b[MVM_MAX_PAIRS];
+};
+
+struct ColRegs {
+    double l0[kColsPerLane], l1[kColsPerLane], l2[kColsPerLane];
+    double x[kColsPerLane], y[kColsPerLane];
+    uint32_t state[kColsPerLane];   // kOk / kDeg / kNone / kWild
+};
+// One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
+// per pair, one 16-byte store, 3 int ops of argmin per pair.
+// MASK: the tail chunk of an aligned matrix (n_b % 4 == 0): a lane's 4 columns
+// are all in the view or all past it (state kNone), and only the former store.
+template <bool ARGMIN, bool STORE, typename OutT, int NT = 1, bool MASK = false>
+__device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
+                                         double rx, double ry, OutT *drow, int jbase, Best &best) {
+    double e[kColsPerLane];
+    float v[kColsPerLane];
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];      // l1 . p1
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;         // l2 . p2
+        const double sum = __builtin_fabs(d1) + __builtin_fabs(d2);
+        if constexpr (sizeof(OutT) == 4) {
+            v[q] = (float)half_for_f32(sum);
+        } else {
+            e[q] = 0.5 * sum;
+        }
+    }
+    if constexpr (sizeof(OutT) == 4) {
+        if (MASK && c.state[0] == kNone) return;
+        if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+        if (ARGMIN) {
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) best_update_fast(best, v[q], jbase + q);
+        }
+    } else {
+        if (STORE) store4_nt(drow + jbase, e);
+    }
+}
+
+// Clean row of a matrix whose rows are not 16-byte aligned (n_b % 4 != 0):
+// the lane holds columns jbase + 64q, so each of the 4 dword stores writes 256
+// contiguous bytes.  Default store policy: a row's first and last lines are
+// shared with its neighbours and L2 merges them (nontemporal partial lines
+// reach HBM as masked writes, ~3.7x slower).
+// Also the tail chunk of any float32 matrix: columns past the view (kNone) are
+// skipped per lane.  drow == nullptr: association only.
+template <bool ARGMIN>
+__device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, double rl1,
+                                                 double rl2, double rx, double ry, float *drow,
+                                                 int jbase, Best &best) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
+        const float v = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
+        if (c.state[q] != kNone) {
+            if (drow) drow[jbase + kWave * q] = v;
+            if (ARGMIN) best_update_fast(best, v, jbase + kWave * q);
+        }
+    }
+}
+
+// Generic row: degenerate lines (9999 sentinel), non-finite or huge values,
+// tails, unaligned rows, no output buffer.  Column of slot q: jbase + q*jstep.
+template <bool ARGMIN, typename OutT>
+__device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl1, double rl2,
+                                         double rx, double ry, bool rdeg, OutT *drow, int jbase,
+                                         int jstep, Best &best) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);
+        d1 = (c.state[q] == kDeg) ? kSentinel : d1;
+        const double d2 = rdeg ? kSentinel : line_dist(rl0, rl1, rl2, c.x[q], c.y[q]);
+        const double e = 0.5 * (d1 + d2);                                            // :28
+        const bool valid = c.state[q] != kNone;
+        const int j = jbase + q * jstep;
+        if (drow && valid) drow[j] = (OutT)e;   // default policy: L2 merges partial lines
+        if (ARGMIN && valid) best_update_safe(best, (float)e, j);
+    }
+}
+
+// ---- lazy argmin (clean row groups) ----
+// In a row group whose rows and columns are all clean (finite, non-degenerate,
+// one column tile), a lane keeps per row only the float32 bits of its minimum
+// (non-negative finite floats order like their bits) and the CHUNK it came
+// from: two v_min3_u32 + one compare + one select per 4 pairs instead of a
+// compare and two selects per pair.  The column inside the chunk is recovered
+// once per group (lane r recomputes the 4 values of row r's winning lane and
+// chunk, `lazy_recover`), so the result is exactly np.argmin's: the earliest
+// chunk wins inside a lane (strict '<'), the lowest q inside a chunk, and
+// rows whose minimum sits in several lanes take the tie path.
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t ab = a < b ? a : b;   // -> v_min3_u32
+    return ab < c ? ab : c;
+}
+
+// float32 bits of the 4 stored values of one lane for one row (row_fast's arithmetic)
+__device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double rl1, double rl2,
+                                           double rx, double ry, float v[kColsPerLane]) {
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
+        const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
+        v[q] = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
+    }
+}
+
+template <bool STORE, int NT>
+__device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
+                                              double rx, double ry, float *drow, int jbase,
+                                              uint32_t &bbits, int32_t &bchunk, int32_t cidx) {
+    float v[kColsPerLane];
+    pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
+    if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+    const uint32_t m = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]),
+                                         __float_as_uint(v[2])),
+                                __float_as_uint(v[3]), bbits);
+    bchunk = (m < bbits) ? cidx : bchunk;
+    bbits = m;
+}
+
+// Column (within the tile) of the first of the 4 values of columns jj0..jj0+3
+// against row line/point `rl`/`rx,ry` whose bits equal `k` (4 if none).
+__device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_l1,
+                                            const double *s_l2, const double *s_x,
+                                            const double *s_y, int jj0, double rl0, double rl1,
+                                            double rl2, double rx, double ry, uint32_t k) {
+    ColRegs c;
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        c.l0[q] = s_l0[jj0 + q];
+        c.l1[q] = s_l1[jj0 + q];
+        c.l2[q] = s_l2[jj0 + q];
+        c.x[q] = s_x[jj0 + q];
+        c.y[q] = s_y[jj0 + q];
+    }
+    float v[kColsPerLane];
+    pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
+    int q = kColsPerLane;
+#pragma unroll
+    for (int p = kColsPerLane - 1; p >= 0; --p) q = (__float_as_uint(v[p]) == k) ? p : q;
+    return q;
+}
+
+// ---- transposed lazy reduction (lazy == 2, the default) ----
+// Minimum over the LPR = 64 / RPW consecutive lanes that share one row slot.
+// Quad xor steps, then row_half_mirror / row_mirror: every lane of the group
+// ends with the group minimum.
+template <int RPW>
+__device__ __forceinline__ uint32_t group_min_u32(uint32_t v) {
+    constexpr int LPR = kWave / RPW;
+    if constexpr (LPR >= 2) v = dpp_min<0xB1>(v);
+    if constexpr (LPR >= 4) v = dpp_min<0x4E>(v);
+    if constexpr (LPR >= 8) v = dpp_min<0x141>(v);
+    if constexpr (LPR >= 16) v = dpp_min<0x140>(v);
+    return v;
+}
+
+// The RPW lane minima of row slot `rs` that segment `seg` owns, from the
+// wave's [RPW][64] LDS scratch (16-byte reads; RPW is a multiple of 4).
+template <int RPW>
+__device__ __forceinline__ void read_segment(const uint32_t *red, int rs, int seg,
+                                             uint32_t (&v)[RPW]) {
+    const uint32_t *src = red + rs * kWave + seg * RPW;
+#pragma unroll
+    for (int i = 0; i < RPW; i += 4) {
+        const uint4 q = *reinterpret_cast<const uint4 *>(src + i);
+        v[i] = q.x;
+        v[i + 1] = q.y;
+        v[i + 2] = q.z;
+        v[i + 3] = q.w;
+    }
+}
+
+// End of a clean (lazy) row group.  Lane L holds, per row slot r, the float32
+// bits of its minimum bbits[r] and the chunk it first reached it in,
+// bchunk[r].  The per-row wave reductions (RPW x (4 DPP + 4 readlane + ballot
+// + selects)) become one transpose through LDS: lane L takes row slot
+// rs = L / LPR and the RPW lanes [seg*RPW, seg*RPW + RPW) of that row
+// (seg = L % LPR), reduces them in registers, and finishes over its LPR lanes
+// with DPP.  The winner is the lowest (chunk, lane) holding the row minimum k
+// -- the lowest column, since column = chunk*256 + 4*lane + q.  Returns k and
+// the winner's lane and chunk, uniform over the LPR lanes of the row slot.
+template <int RPW>
+__device__ __forceinline__ void lazy_reduce_transposed(uint32_t *red, const uint32_t (&bbits)[RPW],
+                                                       const int32_t (&bchunk)[RPW], bool multi,
+                                                       int lane, uint32_t &k, int &w, int &c) {
+    constexpr int LPR = kWave / RPW;
+    const int rs = lane / LPR, seg = lane % LPR;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = bbits[r];
+    // the same wave reads them back: LDS executes one wave's ops in order
+    uint32_t v[RPW];
+    read_segment<RPW>(red, rs, seg, v);
+    uint32_t m = v[0];
+#pragma unroll
+    for (int i = 1; i < RPW; ++i) m = v[i] < m ? v[i] : m;
+    k = group_min_u32<RPW>(m);
+    uint32_t key = 0xFFFFFFFFu;
+    if (!multi) {   // one chunk: the first lane of the segment holding k
+        uint32_t pos = RPW;
+#pragma unroll
+        for (int i = RPW - 1; i >= 0; --i) pos = (v[i] == k) ? (uint32_t)i : pos;
+        key = (pos < (uint32_t)RPW) ? (uint32_t)(seg * RPW) + pos : key;
+    } else {        // several chunks: lowest (chunk, lane) among the lanes holding k
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = (uint32_t)bchunk[r];
+        uint32_t ch[RPW];
+        read_segment<RPW>(red, rs, seg, ch);
+#pragma unroll
+        for (int i = 0; i < RPW; ++i) {
+            const uint32_t ki = (ch[i] << 6) | (uint32_t)(seg * RPW + i);
+            const uint32_t cand = (v[i] == k) ? ki : 0xFFFFFFFFu;
+            key = cand < key ? cand : key;
+        }
+    }
+    key = group_min_u32<RPW>(key);
+    w = (int)(key & 63u);
+    c = (int)(key >> 6);
+}
+
+
+// Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair).  The
+// normalised lines of (up to col_tile) columns are computed ONCE per
+// workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
+// chunk every lane holds 4 consecutive columns in registers and walks the
+// RPW rows, one coalesced 16-byte store per lane per row.
+// occupancy: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
+// (RPW 16 at 4 waves/SIMD spills and measured slower: DESIGN.md §3.1)
+template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
+__global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(PairArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int T = args.col_tile;
+    double *s_l0 = reinterpret_cast<double *>(s_dyn);
+    double *s_l1 = s_l0 + T;
+    double *s_l2 = s_l1 + T;
+    double *s_x = s_l2 + T;
+    double *s_y = s_x + T;
+    // per wave: the row lines of up to 64 rows (all its groups when they fit)
+    double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
+    double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
+    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
+    // lazy == 2: per wave an [RPW][64] u32 scratch for the transposed reduction
+    uint32_t *s_red = s_cst + T;
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
+    const int lane = t % kWave;
+    // dispatch places workgroup b on XCD b % 8; each XCD walks a contiguous
+    // range of (scene, pair, row block)s, so a (scene, pair)'s row blocks
+    // share one L2 and its output region stays contiguous per XCD
+    uint32_t blk = blockIdx.x;
+    {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const int rb = (int)(blk % (uint32_t)args.row_blocks);
+    const int sp = (int)(blk / (uint32_t)args.row_blocks);
+    const int s = sp / args.n_pairs;
+    const int p = sp - s * args.n_pairs;
+    const int cam_a = args.pair_a[p], cam_b = args.pair_b[p];
+    const int64_t oa = args.cam_offs[(int64_t)s * args.n_cams + cam_a];
+    const int na = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_a + 1] - oa);
+    const int64_t ob = args.cam_offs[(int64_t)s * args.n_cams + cam_b];
+    const int nb = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_b + 1] - ob);
+    // rows of the workgroup: [row0, row0 + rows_per_wg)
+    constexpr int U = kWaves * RPW;
+    const int row0 = rb * args.rows_per_wg;
+    if (row0 >= na) return;   // uniform over the workgroup
+
+    double f[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) f[k] = args.F[(int64_t)sp * 9 + k];
+
+    const int64_t doff = args.dist_offs ? args.dist_offs[sp] : (int64_t)sp * args.mat_stride;
+    // first association row of this matrix, loaded before any store (a vector
+    // load issued after the stores would wait for all of them: vmcnt is in order)
+    const int64_t row_off0 = args.row_offs ? args.row_offs[sp] : 0;
+    const int64_t ld = args.ld ? args.ld : nb;
+    OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
+    const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
+    // unaligned float32 rows: lanes take strided columns (coalesced dword stores)
+    const bool strided = dbase && !vec_ok && sizeof(OutT) == 4;
+
+    // column lines of columns [c0, c0 + T) -> LDS (threads stride the tile)
+    auto load_tile = [&](int c0) {
+        for (int jj = t; jj < T; jj += kThreads) {
+            const int j = c0 + jj;
+            uint32_t st = kNone;
+            double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+            if (j < nb) {
+                x = args.pts[2 * (ob + j)];
+                y = args.pts[2 * (ob + j) + 1];
+                st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
+            }
+            s_l0[jj] = l0;
+            s_l1[jj] = l1;
+            s_l2[jj] = l2;
+            s_x[jj] = x;
+            s_y[jj] = y;
+            s_cst[jj] = st;
+        }
+    };
+    // every global load of the workgroup's rows happens here, before the first
+    // store (on CDNA vmcnt orders loads behind earlier stores)
+    for (int x = t; x < args.rows_per_wg; x += kThreads) {
+        const int i = row0 + x;
+        const f64x2 v = (i < na) ? *reinterpret_cast<const f64x2 *>(args.pts + 2 * (oa + i))
+                                 : f64x2{0.0, 0.0};
+        *reinterpret_cast<f64x2 *>(s_rpt + 2 * x) = v;
+    }
+    const int n_tiles = (nb + T - 1) / T;
+    if (n_tiles == 1) load_tile(0);
+    // lazy argmin needs every column of the (single) tile clean
+    bool my_clean = n_tiles == 1;
+    if (ARGMIN && sizeof(OutT) == 4 && args.lazy && n_tiles == 1)
+        for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] == kOk);
+    const bool tile_clean = __syncthreads_and(my_clean) != 0;
+
+    const int n_groups = (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
+    // group g's geometry: first local row, matrix row, rows
+    auto group_rows = [&](int g, int &xw, int &grow0, int &nrows) {
+        xw = (g * kWaves + wave) * RPW;
+        grow0 = row0 + xw;
+        nrows = min(RPW, na - grow0);                          // may be <= 0
+    };
+    // line of local row xw + row into slot `slot` of the wave's LDS rows
+    auto put_row_line = [&](int slot, int xw, int row, int nrows) {
+        double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+        bool deg = true;
+        if (row < nrows) {
+            x = s_rpt[2 * (xw + row)];
+            y = s_rpt[2 * (xw + row) + 1];
+            deg = row_line(f, x, y, l0, l1, l2);
+        }
+        s_row[wave][slot][0] = l0;
+        s_row[wave][slot][1] = l1;
+        s_row[wave][slot][2] = l2;
+        s_row[wave][slot][3] = x;
+        s_row[wave][slot][4] = y;
+        s_row[wave][slot][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
+    };
+    // all of the wave's groups fit in 64 rows: one lane per row computes every
+    // row line up front (one pass instead of one 16-lane pass per group)
+    const bool pre = RPW * n_groups <= kWave;   // uniform
+    if (pre && lane < RPW * n_groups) {
+        int xw, grow0, nrows;
+        const int g = lane / RPW, slot = lane % RPW;
+        group_rows(g, xw, grow0, nrows);
+        put_row_line(lane, xw, slot, nrows);
+    }
+    for (int g = 0; g < n_groups; ++g) {
+        int xw, grow0, nrows;
+        group_rows(g, xw, grow0, nrows);
+        double(*rowp)[6] = s_row[wave] + (pre ? g * RPW : 0);   // this group's slots
+        if (!pre && lane < RPW)   // row lines of this wave's group (wave-private LDS slots)
+            put_row_line(lane, xw, lane, nrows);
+        // the same wave reads them back (LDS executes one wave's ops in order)
+        const bool rows_fast =
+            (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
+
+        Best best[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) best[r] = Best{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+        // uniform: the whole group takes the lazy argmin (clean rows and tile)
+        const bool lazy = ARGMIN && sizeof(OutT) == 4 && args.lazy && args.row_offs &&
+                          tile_clean && rows_fast && (vec_ok || !dbase);
+        if (lazy) {
+            uint32_t bbits[RPW];
+            int32_t bchunk[RPW];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                bbits[r] = 0x7F800000u;
+                bchunk[r] = 0;
+            }
+            for (int c0 = 0, cidx = 0; c0 < nb; c0 += kChunk, ++cidx) {
+                ColRegs c;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = c0 + kColsPerLane * lane + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
+                }
+                const int jbase = c0 + kColsPerLane * lane;
+                if (dbase) {
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1],
+                                                rowp[r][2], rowp[r][3],
+                                                rowp[r][4], reinterpret_cast<float *>(rp),
+                                                jbase, bbits[r], bchunk[r], cidx);
+                        rp += rstep;
+                        // keep the row address a running scalar: stops LICM
+                        // hoisting all RPW row bases out of the chunk loop
+                        // (they would be spilled to VGPR lanes)
+                        __asm__ volatile("" : "+s"(rp));
+                    }
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast_lazy<false, NT>(c, rowp[r][0], rowp[r][1],
+                                                 rowp[r][2], rowp[r][3],
+                                                 rowp[r][4], nullptr, jbase, bbits[r],
+                                                 bchunk[r], cidx);
+                }
+            }
+            if (args.lazy >= 2) {
+                constexpr int LPR = kWave / RPW;
+                uint32_t k;
+                int w, cw;
+                lazy_reduce_transposed<RPW>(s_red + wave * (RPW * kWave), bbits, bchunk,
+                                            nb > kChunk, lane, k, w, cw);
+                // the LPR lanes of row slot rs recompute the winner's 4 values
+                // (lane seg takes q = seg % 4) and keep the first equal to k
+                const int rs = lane / LPR, q = (lane % LPR) & (kColsPerLane - 1);
+                const int jj = cw * kChunk + kColsPerLane * w + q;
+                const double *rl = rowp[rs];
+                const double d1 = __builtin_fma(s_l1[jj], rl[4], s_l0[jj] * rl[3]) + s_l2[jj];
+                const double d2 = __builtin_fma(rl[1], s_y[jj], rl[0] * s_x[jj]) + rl[2];
+                const uint32_t b =
+                    __float_as_uint((float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2)));
+                const uint32_t qm = group_min_u32<RPW>((b == k) ? (uint32_t)q : 0xFFFFFFFFu);
+                if (lane % LPR == 0) {
+                    const int64_t row = row_off0 + grow0 + rs;
+                    if (args.argmin) args.argmin[row] = jj - q + (int)qm;
+                    if (args.minval) args.minval[row] = __uint_as_float(k);
+                }
+                continue;
+            }
+            // per row: wave minimum, its lane and chunk; lane r gathers row r's
+            uint32_t my_k = 0;
+            int32_t my_l = 0, my_c = 0;
+            uint32_t ties = 0;   // rows whose minimum sits in several lanes
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {
+                const uint32_t k = wave_min_u32(bbits[r]);
+                const uint64_t hit = __ballot(bbits[r] == k);
+                const int wl = (int)__builtin_ctzll(hit);
+                ties |= (__builtin_popcountll(hit) > 1) ? (1u << r) : 0u;
+                const int wc = __builtin_amdgcn_readlane(bchunk[r], wl);
+                my_k = (lane == r) ? k : my_k;
+                my_l = (lane == r) ? wl : my_l;
+                my_c = (lane == r) ? wc : my_c;
+            }
+            int32_t my_j = 0;
+            if (lane < RPW) {   // lane r recovers the column of row slot r
+                const int jj0 = my_c * kChunk + kColsPerLane * my_l;
+                my_j = jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0, rowp[lane][0],
+                                          rowp[lane][1], rowp[lane][2],
+                                          rowp[lane][3], rowp[lane][4], my_k);
+            }
+            if (ties) {
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) {
+                    if (!(ties & (1u << r))) continue;   // uniform
+                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)my_k, r);
+                    uint32_t cand = 0x7FFFFFFFu;
+                    if (bbits[r] == k) {   // every lane holding the minimum finds its first column
+                        const int jj0 = bchunk[r] * kChunk + kColsPerLane * lane;
+                        cand = (uint32_t)(jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0,
+                                                             rowp[r][0], rowp[r][1],
+                                                             rowp[r][2], rowp[r][3],
+                                                             rowp[r][4], k));
+                    }
+                    const int32_t jt = (int32_t)wave_min_u32(cand);
+                    my_j = (lane == r) ? jt : my_j;
+                }
+            }
+            if (lane < nrows) {
+                const int64_t row = row_off0 + grow0 + lane;
+                if (args.argmin) args.argmin[row] = my_j;
+                if (args.minval) args.minval[row] = __uint_as_float(my_k);
+            }
+            continue;
+        }
+
+        for (int tile = 0; tile < n_tiles; ++tile) {
+            if (n_tiles > 1) {   // large views: stream the column lines tile by tile
+                __syncthreads();
+                load_tile(tile * T);
+                __syncthreads();
+            }
+            const int tile_cols = min(T, nb - tile * T);
+            if (nrows <= 0) continue;
+            for (int c0 = 0; c0 < tile_cols; c0 += kChunk) {
+                // strided columns for unaligned rows; an aligned matrix's tail chunk
+                // keeps 16-byte stores, masked per lane
+                const bool str = strided;
+                const bool tail = sizeof(OutT) == 4 && c0 + kChunk > tile_cols;
+                ColRegs c;
+                bool clean = true, clean_m = true;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = str ? c0 + lane + kWave * q : c0 + kColsPerLane * lane + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
+                    c.state[q] = s_cst[jj];
+                    clean &= (c.state[q] == kOk);
+                    clean_m &= (c.state[q] == kOk || c.state[q] == kNone);
+                }
+                const int jbase = tile * T + c0 + (str ? lane : kColsPerLane * lane);
+                const int jstep = str ? kWave : 1;
+                const bool fast = rows_fast && __all(clean);   // wave-uniform
+                if (str && rows_fast && __all(clean_m)) {   // clean rows: unaligned output or tail
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast_strided<ARGMIN>(c, rowp[r][0], rowp[r][1],
+                                                 rowp[r][2], rowp[r][3],
+                                                 rowp[r][4],
+                                                 dbase ? reinterpret_cast<float *>(dbase + (int64_t)(grow0 + r) * ld)
+                                                       : nullptr,
+                                                 jbase, best[r]);
+                    }
+                } else if (tail && vec_ok && rows_fast && __all(clean_m)) {   // aligned tail chunk
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    const uint64_t rbase = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast<ARGMIN, true, OutT, NT, true>(
+                            c, rowp[r][0], rowp[r][1], rowp[r][2],
+                            rowp[r][3], rowp[r][4],
+                            reinterpret_cast<OutT *>(rbase + (uint64_t)r * rstep), jbase, best[r]);
+                    }
+                } else if (fast && vec_ok) {   // the common case: clean rows, aligned output
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast<ARGMIN, true, OutT, NT>(c, rowp[r][0], rowp[r][1],
+                                               rowp[r][2], rowp[r][3],
+                                               rowp[r][4], reinterpret_cast<OutT *>(rp),
+                                               jbase, best[r]);
+                        rp += rstep;
+                        // keep the row address a running scalar: stops LICM
+                        // hoisting all RPW row bases out of the chunk loop
+                        // (they would be spilled to VGPR lanes)
+                        __asm__ volatile("" : "+s"(rp));
+                    }
+                } else if (fast && !dbase) {   // association only, no matrix output
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast<ARGMIN, false, OutT>(c, rowp[r][0], rowp[r][1],
+                                                      rowp[r][2], rowp[r][3],
+                                                      rowp[r][4], nullptr, jbase, best[r]);
+                } else {
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        if (r < nrows) {
+                            OutT *drow = dbase ? dbase + (int64_t)(grow0 + r) * ld : nullptr;
+                            const bool rdeg = __builtin_amdgcn_readfirstlane(
+                                                  (int)rowp[r][5]) == (int)kDeg;
+                            row_safe<ARGMIN>(c, rowp[r][0], rowp[r][1],
+                                             rowp[r][2], rowp[r][3],
+                                             rowp[r][4], rdeg, drow, jbase, jstep, best[r]);
+                        }
+                    }
+                }
+            }
+        }
+
+        if (ARGMIN && args.row_offs && nrows > 0) {
+            uint32_t kmin[RPW];
+            int32_t imin[RPW];
+#pragma unroll
+            for (int r = 0; r < RPW; ++r) {   // independent DPP chains interleave
+                kmin[r] = kKeyInvalid;
+                imin[r] = 0;
+                if (r < nrows) wave_argmin(best_key(best[r]), best[r].j, kmin[r], imin[r]);
+            }
+            store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                                   row_off0 + grow0);
+        }
+    }
+}
+
+// ------------------------------------------------------------ host side ----
+constexpr int kRowsPerWave = 16;    // default: 64 rows per row group
+constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
+
+int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
+               int n_cams) {
+    if (n_cams < 2 || n_cams > MVM_MAX_CAMS)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "n_cams=%d outside [2, %d]", n_cams, MVM_MAX_CAMS);
+    if (n_pairs < 1 || n_pairs > MVM_MAX_PAIRS)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "n_pairs=%d outside [1, %d]", n_pairs, MVM_MAX_PAIRS);
+    if (!pair_a || !pair_b) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pair list");
+    for (int p = 0; p < n_pairs; ++p) {
+        if (pair_a[p] < 0 || pair_a[p] >= n_cams || pair_b[p] < 0 || pair_b[p] >= n_cams ||
+            pair_a[p] == pair_b[p])
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pair %d = (%d, %d) invalid for %d cameras",
+                            p, pair_a[p], pair_b[p], n_cams);
+        a.pair_a[p] = pair_a[p];
+        a.pair_b[p] = pair_b[p];
+    }
+    a.n_cams = n_cams;
+    a.n_pairs = n_pairs;
+    return MVM_OK;
+}
+
+template <int RPW>
+size_t pairwise_lds_bytes(int col_tile, int rows_per_wg, bool transposed_reduction) {
+    return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
+           (size_t)kWaves * kWave * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double) +
+           (transposed_reduction ? (size_t)kWaves * RPW * kWave * sizeof(uint32_t) : 0);
+}
+
+// Launch with `lds` bytes of dynamic LDS (above 64 KiB the kernel must opt in).
+template <typename Kernel>
+int launch_lds(Kernel kern, dim3 grid, dim3 block, size_t lds, hipStream_t stream,
+               const PairArgs &a) {
+    if (lds > 65536 &&
+        hipFuncSetAttribute(reinterpret_cast<const void *>(kern),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+    kern<<<grid, block, lds, stream>>>(a);
+    return MVM_OK;
+}
+
+template <int RPW>
+int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_cols,
+                        int row_groups, bool argmin, bool f64, hipStream_t stream) {
+    a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
+    a.rows_per_wg = kWaves * RPW * row_groups;
+    a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
+    const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, argmin && !f64 && a.lazy >= 2);
+    if (f64) return launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
+    // nontemporal stores for whole-line rows; rows that end mid-line share
+    // that line with the next row, and L2 must merge it (default policy)
+    if (max_cols % 32 == 0) {
+        if (argmin) return launch_lds(pairwise_kernel<RPW, true, float, 1>, grid, block, lds, stream, a);
+        return launch_lds(pairwise_kernel<RPW, false, float, 1>, grid, block, lds, stream, a);
+    }
+    if (argmin) return launch_lds(pairwise_kernel<RPW, true, float, 0>, grid, block, lds, stream, a);
+    return launch_lds(pairwise_kernel<RPW, false, float, 0>, grid, block, lds, stream, a);
+}
+
+int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int32_t max_cols,
+                           bool argmin, bool f64, const mvm_options &o, hipStream_t stream) {
+    if (n_scenes < 0 || max_rows < 0 || max_cols < 0)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_scenes/max_rows/max_cols");
+    if (n_scenes == 0 || max_rows == 0) return MVM_OK;
+    switch (o.pairwise_argmin) {
+    case MVM_PAIRWISE_ARGMIN_DEFAULT:
+    case MVM_PAIRWISE_ARGMIN_LAZY_TRANSPOSED: a.lazy = 2; break;
+    case MVM_PAIRWISE_ARGMIN_LAZY_ROWS: a.lazy = 1; break;
+    case MVM_PAIRWISE_ARGMIN_EAGER: a.lazy = 0; break;
+    default: return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_argmin %d", (int)o.pairwise_argmin);
+    }
+    const int rpw = o.pairwise_rows_per_wave ? o.pairwise_rows_per_wave : kRowsPerWave;
+    if (rpw != 4 && rpw != 8 && rpw != 16)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_rows_per_wave %d not 4, 8 or 16", rpw);
+    if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
+                        (int)o.pairwise_row_groups);
+    // default: enough row groups to amortise the column lines over >= ~256
+    // rows, but never more than the rows a view has
+    const int groups_needed = (max_rows + kWaves * rpw - 1) / (kWaves * rpw);
+    const int rg = o.pairwise_row_groups ? o.pairwise_row_groups
+                                         : max(1, min(groups_needed, 256 / (kWaves * rpw)));
+    const int64_t sp_count = (int64_t)n_scenes * a.n_pairs;
+    const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
+    const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
+    if (blocks > 0x7FFFFFFFLL)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
+                        (long long)blocks);
+    int st;
+    switch (rpw) {
+    case 4: st = launch_pairwise_rpw<4>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
+    case 8: st = launch_pairwise_rpw<8>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
+    default: st = launch_pairwise_rpw<16>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
+    }
+    return st ? st : mvm_check_launch("pairwise_kernel");
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
+                                    const double *F_dev, const int32_t *pair_a,
+                                    const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                    int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
+                                    const int64_t *row_offs_dev, float *dist_dev,
+                                    int32_t *argmin_dev, float *minval_dev,
+                                    const mvm_options *opts, mvm_stream_t stream) {
+    mvm_clear_error();
+    mvm_options o;
+    int st = mvm_resolve_options(opts, o);
+    if (st) return st;
+    PairArgs a{};
+    st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
+    if (st) return st;
+    if (n_scenes > 0 && max_n > 0 && (!pts_dev || !cam_offs_dev || !F_dev))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null input pointer");
+    if (dist_dev && !dist_offs_dev) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "dist without dist_offs");
+    if ((argmin_dev || minval_dev) && !row_offs_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "argmin/minval without row_offs");
+    a.pts = pts_dev;
+    a.cam_offs = cam_offs_dev;
+    a.F = F_dev;
+    a.dist_offs = dist_offs_dev;
+    a.row_offs = row_offs_dev;
+    a.dist = dist_dev;
+    a.argmin = argmin_dev;
+    a.minval = minval_dev;
+    a.ld = 0;
+    const bool want_argmin = argmin_dev || minval_dev;
+    return launch_pairwise_common(a, n_scenes, max_n, max_n, want_argmin, false, o,
+                                  reinterpret_cast<hipStream_t>(stream));
+}
+
+int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
+                                 const double *F_dev, const int32_t *pair_a,
+                                 const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                 int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
+                                 const int64_t *row_offs_dev, float *dist_dev,
+                                 int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream) {
+    return mvm_pairwise_residual_argmin_ex(pts_dev, cam_offs_dev, F_dev, pair_a, pair_b, n_scenes,
+                                           n_cams, n_pairs, max_n, dist_offs_dev, row_offs_dev,
+                                           dist_dev, argmin_dev, minval_dev, nullptr, stream);
+}
+
+int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev,
+                              const double *F_dev, const int32_t *pair_a, const int32_t *pair_b,
+                              int32_t n_scenes, int32_t n_cams, int32_t n_pairs,
+                              int32_t max_n, int64_t mat_stride, int64_t ld, double *e_dev,
+                              mvm_stream_t stream) {
+    mvm_clear_error();
+    PairArgs a{};
+    int st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
+    if (st) return st;
+    if (n_scenes > 0 && max_n > 0 && (!pts_dev || !cam_offs_dev || !F_dev || !e_dev))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (ld <= 0 || mat_stride < 0)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "ld must be > 0 and mat_stride >= 0");
+    a.pts = pts_dev;
+    a.cam_offs = cam_offs_dev;
+    a.F = F_dev;
+    a.dist = e_dev;
+    a.mat_stride = mat_stride;
+    a.ld = ld;
+    mvm_options o;
+    mvm_options_init(&o);
+    return launch_pairwise_common(a, n_scenes, max_n, max_n, false, true, o,
+                                  reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

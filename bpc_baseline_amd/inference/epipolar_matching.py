@@ -139,13 +139,21 @@ _LSAP_ERRORS = {1: "matrix contains invalid numeric entries", 2: "cost matrix is
 
 
 def linear_sum_assignment(cost_matrix):
-    """GPU ``scipy.optimize.linear_sum_assignment`` for one matrix -> (row_ind, col_ind)."""
+    """GPU ``scipy.optimize.linear_sum_assignment`` for one matrix -> (row_ind, col_ind).
+
+    scipy converts any input to float64 before assigning; a float32 matrix
+    converts exactly, so it is assigned in its own type (half the bytes),
+    every other dtype is converted to float64 as scipy does and assigned in
+    float64 (``mvm_lsap_solve_ex`` with MVM_F64)."""
     dev = _device()
-    cost = np.ascontiguousarray(np.asarray(cost_matrix, dtype=np.float32))
+    arr = np.asarray(cost_matrix)
+    dt = np.float32 if arr.dtype == np.float32 else np.float64
+    cost = np.ascontiguousarray(arr, dtype=dt)
     if cost.ndim != 2:
         raise ValueError("expected a matrix")
-    plan = ops.LsapPlan([cost.shape[0]], [cost.shape[1]], device=dev)
-    cost_d = torch.from_numpy(cost.reshape(-1) if cost.size else np.zeros(1, np.float32)).to(dev)
+    tdt = torch.float32 if dt == np.float32 else torch.float64
+    plan = ops.LsapPlan([cost.shape[0]], [cost.shape[1]], device=dev, dtype=tdt)
+    cost_d = torch.from_numpy(cost.reshape(-1) if cost.size else np.zeros(1, dt)).to(dev)
     offs = torch.zeros(1, dtype=torch.int64, device=dev)
     r, c, st = ops.linear_sum_assignment_batched(cost_d, offs, plan)
     status = int(st.cpu()[0])
@@ -158,9 +166,9 @@ def match_objects(cost_matrix, threshold) -> List[Tuple[int, int, int]]:
     """Flatten -> Hungarian -> keep matches < threshold (epipolar_matching.py:100-116).
 
     The assignment runs on the GPU and equals scipy ``linear_sum_assignment``
-    on the ``(N*M, P)`` flattening; strict ``<`` threshold; ``i = r // M``,
-    ``j = r % M``.  Non-float32 cubes are assigned in float32, the dtype
-    compute_cost_matrix returns.
+    on the ``(N*M, P)`` flattening, in the precision scipy uses for the
+    cube's dtype; strict ``<`` threshold on the cube's own values;
+    ``i = r // M``, ``j = r % M``.
     """
     N, M, P = cost_matrix.shape
     flat = cost_matrix.reshape(N * M, P)

@@ -12,6 +12,12 @@ Ops (all ``*_out`` ops write caller-allocated tensors, like the C ABI):
 Plans (``PairwisePlan`` / ``TripletPlan``) hold the host-side offset tables
 (prefix sums of the per-view detection counts) and their device copies; a
 plan is reusable for every batch with the same counts.
+
+Kernel-path choices (``include/mvmatch.h`` ``mvm_options``) are explicit:
+the high-level functions take ``options=dict(...)`` (field names of
+``_native.MvmOptions``) and the ops an ``opts`` list of the field values; by
+default (None) the library's compiled-in defaults apply.  The choices never
+change results -- the parity tests run every path.
 """
 from __future__ import annotations
 
@@ -48,6 +54,21 @@ def _h2d_int64(arrays: List[np.ndarray], device: torch.device) -> List[Tensor]:
         out.append(dev[o:o + a.size])
         o += a.size
     return out
+
+
+def _opts_list(options: Optional[dict]) -> Optional[List[int]]:
+    """options dict -> the op's ``opts`` list (mvm_options fields after ``size``)."""
+    o = _native.make_options(**(options or {}))
+    return None if o is None else [int(getattr(o, n)) for n in _native.OPTION_FIELDS]
+
+
+def _opts_ref(opts: Optional[List[int]]):
+    """The op's ``opts`` list -> a pointer to an mvm_options (None = defaults)."""
+    if opts is None:
+        return None
+    if len(opts) != len(_native.OPTION_FIELDS):
+        raise ValueError(f"opts: expected {len(_native.OPTION_FIELDS)} values, got {len(opts)}")
+    return ctypes.byref(_native.make_options(**dict(zip(_native.OPTION_FIELDS, opts))))
 
 
 def _p(t: Optional[Tensor]):
@@ -90,7 +111,8 @@ def _check_inputs(pts: Tensor, cam_offs: Tensor, F: Tensor, n_views: int, n_mats
 def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_a: List[int],
                                  pair_b: List[int], n_scenes: int, n_cams: int, max_n: int,
                                  dist_offs: Tensor, row_offs: Tensor, dist: Tensor,
-                                 argmin: Tensor, minval: Tensor) -> None:
+                                 argmin: Tensor, minval: Tensor,
+                                 opts: Optional[List[int]] = None) -> None:
     n_pairs = len(pair_a)
     _check_inputs(pts, cam_offs, F, n_scenes * n_cams, n_scenes * n_pairs)
     for t, n, dt in ((dist_offs, "dist_offs", torch.int64), (row_offs, "row_offs", torch.int64),
@@ -99,15 +121,16 @@ def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_
         _require(t, n, dt, pts.device)
     pa = (ctypes.c_int32 * n_pairs)(*pair_a)
     pb = (ctypes.c_int32 * n_pairs)(*pair_b)
-    st = _native.load().mvm_pairwise_residual_argmin(
+    st = _native.load().mvm_pairwise_residual_argmin_ex(
         _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_n,
-        _p(dist_offs), _p(row_offs), _p(dist), _p(argmin), _p(minval), _stream(pts))
-    _native.check("mvm_pairwise_residual_argmin", st)
+        _p(dist_offs), _p(row_offs), _p(dist), _p(argmin), _p(minval), _opts_ref(opts),
+        _stream(pts))
+    _native.check("mvm_pairwise_residual_argmin_ex", st)
 
 
 @pairwise_residual_argmin_out.register_fake
 def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_n, dist_offs, row_offs, dist,
-      argmin, minval):
+      argmin, minval, opts=None):
     return None
 
 
@@ -137,21 +160,23 @@ def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_n, mat_stride, ld,
                          mutates_args=("cube", "argmin", "minval", "workspace"))
 def triplet_cost_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, max_n: int,
                             cube_offs: Tensor, row_offs: Tensor, cube: Tensor, argmin: Tensor,
-                            minval: Tensor, workspace: Tensor) -> None:
+                            minval: Tensor, workspace: Tensor,
+                            opts: Optional[List[int]] = None) -> None:
     _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
     for t, n, dt in ((cube_offs, "cube_offs", torch.int64), (row_offs, "row_offs", torch.int64),
                      (cube, "cube", torch.float32), (argmin, "argmin", torch.int32),
                      (minval, "minval", torch.float32), (workspace, "workspace", torch.uint8)):
         _require(t, n, dt, pts.device)
     ws_bytes = workspace.numel()
-    st = _native.load().mvm_triplet_cost_argmin(
+    st = _native.load().mvm_triplet_cost_argmin_ex(
         _p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(cube_offs), _p(row_offs), _p(cube),
-        _p(argmin), _p(minval), _p(workspace), ws_bytes, _stream(pts))
-    _native.check("mvm_triplet_cost_argmin", st)
+        _p(argmin), _p(minval), _p(workspace), ws_bytes, _opts_ref(opts), _stream(pts))
+    _native.check("mvm_triplet_cost_argmin_ex", st)
 
 
 @triplet_cost_argmin_out.register_fake
-def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minval, workspace):
+def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minval, workspace,
+      opts=None):
     return None
 
 
@@ -159,27 +184,31 @@ def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minv
                          mutates_args=("workspace", "row_ind", "col_ind", "status"))
 def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
                    out_offs: Tensor, workspace: Tensor, row_ind: Tensor, col_ind: Tensor,
-                   status: Tensor, long_min: int = 1, long_max: int = 2 ** 62) -> None:
+                   status: Tensor, long_min: int = 1, long_max: int = 2 ** 62,
+                   opts: Optional[List[int]] = None) -> None:
     dev = cost.device
     if dev.type != "cuda":
         raise ValueError("cost must be a GPU tensor (the matcher has no CPU path)")
-    for t, n, dt in ((cost, "cost", torch.float32), (cost_offs, "cost_offs", torch.int64),
+    if cost.dtype not in (torch.float32, torch.float64):
+        raise ValueError(f"cost: expected float32 or float64, got {cost.dtype}")
+    for t, n, dt in ((cost, "cost", cost.dtype), (cost_offs, "cost_offs", torch.int64),
                      (dims, "dims", torch.int64), (ws_offs, "ws_offs", torch.int64),
                      (out_offs, "out_offs", torch.int64), (workspace, "workspace", torch.uint8),
                      (row_ind, "row_ind", torch.int64), (col_ind, "col_ind", torch.int64),
                      (status, "status", torch.int32)):
         _require(t, n, dt, dev)
     n = status.numel()
-    st = _native.load().mvm_lsap_solve_bounded(_p(cost), _p(cost_offs), _p(dims), n, _p(ws_offs),
-                                               _p(out_offs), _p(workspace), workspace.numel(),
-                                               _p(row_ind), _p(col_ind), _p(status), long_min,
-                                               long_max, _stream(cost))
-    _native.check("mvm_lsap_solve_bounded", st)
+    dtype = _native.MVM_F64 if cost.dtype == torch.float64 else _native.MVM_F32
+    st = _native.load().mvm_lsap_solve_ex(_p(cost), dtype, _p(cost_offs), _p(dims), n, _p(ws_offs),
+                                          _p(out_offs), _p(workspace), workspace.numel(),
+                                          _p(row_ind), _p(col_ind), _p(status), long_min,
+                                          long_max, _opts_ref(opts), _stream(cost))
+    _native.check("mvm_lsap_solve_ex", st)
 
 
 @lsap_solve_out.register_fake
 def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, long_min=1,
-      long_max=2 ** 62):
+      long_max=2 ** 62, opts=None):
     return None
 
 
@@ -331,8 +360,10 @@ class PairwisePlan:
 
 def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: PairwisePlan, *,
                              want_dist: bool = True,
-                             out: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
-    """-> (dist f32 [plan.n_dist], argmin i32 [plan.n_rows], minval f32 [plan.n_rows])."""
+                             out: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
+                             options: Optional[dict] = None):
+    """-> (dist f32 [plan.n_dist], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
+    ``options``: mvm_options fields, e.g. ``{"pairwise_argmin": "eager"}``."""
     dev = pts.device
     if out is None:
         dist = torch.empty(plan.n_dist if want_dist else 0, dtype=torch.float32, device=dev)
@@ -342,7 +373,7 @@ def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: Pai
         dist, argmin, minval = out
     torch.ops.mvmatch.pairwise_residual_argmin_out(
         pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_n,
-        plan.dist_offs, plan.row_offs, dist, argmin, minval)
+        plan.dist_offs, plan.row_offs, dist, argmin, minval, _opts_list(options))
     return dist, argmin, minval
 
 
@@ -385,8 +416,10 @@ class TripletPlan:
 
 def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
                         want_cube: bool = True,
-                        out: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
-    """-> (cube f32 [plan.n_cube], argmin i32 [plan.n_rows], minval f32 [plan.n_rows])."""
+                        out: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
+                        options: Optional[dict] = None):
+    """-> (cube f32 [plan.n_cube], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
+    ``options``: mvm_options fields, e.g. ``{"cube_kernel": "workspace"}``."""
     dev = pts.device
     if out is None:
         cube = torch.empty(plan.n_cube if want_cube else 0, dtype=torch.float32, device=dev)
@@ -396,7 +429,7 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
         cube, argmin, minval = out
     torch.ops.mvmatch.triplet_cost_argmin_out(
         pts, cam_offs, F, plan.n_scenes, plan.max_n, plan.cube_offs, plan.row_offs, cube, argmin,
-        minval, plan.workspace)
+        minval, plan.workspace, _opts_list(options))
     return cube, argmin, minval
 
 
@@ -410,18 +443,25 @@ def hbm_write_probe(buf: Tensor) -> None:
 
 
 class LsapPlan:
-    """Workspace / output layout of a batch of assignment problems (host dims)."""
+    """Workspace / output layout of a batch of assignment problems (host dims)
+    whose costs are ``dtype`` (float32, or float64 as scipy assigns a float64
+    matrix: the workspace holds transposed costs of that type)."""
 
-    def __init__(self, rows, cols, device: torch.device | str = "cuda"):
+    def __init__(self, rows, cols, device: torch.device | str = "cuda",
+                 dtype: torch.dtype = torch.float32):
         rows = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1)
         cols = np.ascontiguousarray(cols, dtype=np.int64).reshape(-1)
+        if dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"LsapPlan: dtype must be float32 or float64, got {dtype}")
         n = rows.size
         ws_offs = np.zeros(n + 1, np.int64)
         out_offs = np.zeros(n + 1, np.int64)
-        total = _native.load().mvm_lsap_plan(n, rows.ctypes.data, cols.ctypes.data,
-                                             ws_offs.ctypes.data, out_offs.ctypes.data)
+        code = _native.MVM_F64 if dtype == torch.float64 else _native.MVM_F32
+        total = _native.load().mvm_lsap_plan_ex(n, rows.ctypes.data, cols.ctypes.data, code,
+                                                ws_offs.ctypes.data, out_offs.ctypes.data)
         if total < 0:
-            raise _native.MvmError("mvm_lsap_plan", -1, _native.load().mvm_last_error_string().decode())
+            raise _native.MvmError("mvm_lsap_plan_ex", -1, _native.load().mvm_last_error_string().decode())
+        self.dtype = dtype
         self.n = n
         self.rows, self.cols = rows, cols
         self.out_offs_host = out_offs
@@ -435,16 +475,20 @@ class LsapPlan:
         self.long_max = int(longs.max()) if longs.size else 0
 
 
-def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan):
+def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan, *,
+                                  options: Optional[dict] = None):
     """scipy.optimize.linear_sum_assignment for every problem of ``plan`` on the GPU.
-    -> (row_ind i64 [n_out], col_ind i64 [n_out], status i32 [n]) device tensors."""
+    -> (row_ind i64 [n_out], col_ind i64 [n_out], status i32 [n]) device tensors.
+    ``cost`` must have the plan's dtype."""
+    if cost.dtype != plan.dtype:
+        raise ValueError(f"cost is {cost.dtype} but the plan was built for {plan.dtype}")
     dev = cost.device
     row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
                                      plan.workspace, row_ind, col_ind, status, plan.long_min,
-                                     plan.long_max)
+                                     plan.long_max, _opts_list(options))
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
 
 

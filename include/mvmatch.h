@@ -17,6 +17,8 @@
  *     nothing is synchronised: results are ready when the stream reaches them;
  *   - no allocation, no host<->device copy and no global mutable state in any
  *     launch function (safe to capture in a hipGraph, re-entrant per stream);
+ *     the library reads no environment variables: kernel-path choices come
+ *     only from an explicit mvm_options argument (the *_ex entry points);
  *   - return value: MVM_OK or an MVM_ERR_* code; mvm_last_error_string()
  *     gives a per-thread message for the last failing call.
  *
@@ -37,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 1
+#define MVM_ABI_VERSION 2
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -51,12 +53,65 @@ enum {
     MVM_ERR_HIP = 4               /* a HIP runtime call or kernel launch failed */
 };
 
+/* Element types of mvm_lsap_*_ex cost matrices. */
+enum { MVM_F32 = 0, MVM_F64 = 1 };
+
 /* Library version string ("mvmatch <semver> gfx950"). */
 const char *mvm_version(void);
 /* Message of the last failing call on this thread ("" if none). */
 const char *mvm_last_error_string(void);
 /* Static description of a status code. */
 const char *mvm_status_string(int status);
+
+/*
+ * Kernel-path selection.  Every choice below selects among kernels that
+ * compute the SAME outputs bit for bit (the parity tests run each path); none
+ * changes what is computed, only how.  The plain entry points use the
+ * compiled-in defaults, which are what mvm_options_init writes (every field
+ * 0 = "default"); the *_ex entry points take a const mvm_options * (NULL =
+ * defaults).  `size` must be sizeof(mvm_options) as the caller compiled it
+ * (mvm_options_init sets it), so the struct can grow without breaking callers.
+ */
+enum {
+    MVM_PAIRWISE_ARGMIN_DEFAULT = 0,     /* = LAZY_TRANSPOSED */
+    MVM_PAIRWISE_ARGMIN_LAZY_TRANSPOSED, /* clean row groups: per-chunk minimum bits,
+                                            one LDS transpose per row group */
+    MVM_PAIRWISE_ARGMIN_LAZY_ROWS,       /* ... with per-row DPP reductions */
+    MVM_PAIRWISE_ARGMIN_EAGER            /* best value + index per pair */
+};
+enum {
+    MVM_CUBE_DEFAULT = 0,   /* by the batch's largest view: SMALL <= 44, FUSED above */
+    MVM_CUBE_SMALL,         /* one workgroup per scene (views < 64; FUSED otherwise) */
+    MVM_CUBE_FUSED,         /* 16 i x 32 j tiles, pair residuals in the prologue
+                               (views <= 256; k-chunked above) */
+    MVM_CUBE_WORKSPACE,     /* fp64 pair matrices to the workspace, then tiles
+                               (views <= 256; GENERIC above) */
+    MVM_CUBE_GENERIC        /* fp64 workspace + one (i, j) row per wave */
+};
+typedef struct mvm_options {
+    int32_t size;                   /* sizeof(mvm_options) */
+    int32_t pairwise_argmin;        /* MVM_PAIRWISE_ARGMIN_* */
+    int32_t pairwise_rows_per_wave; /* 0 default (16); 4, 8 or 16 */
+    int32_t pairwise_row_groups;    /* 0 default (~256 rows per workgroup); 1..16 */
+    int32_t cube_kernel;            /* MVM_CUBE_* */
+    int32_t cube_rows_per_instr;    /* FUSED: 0 default (by view size); 1, 2 or 4
+                                       (i, j) rows per wave instruction, capped by
+                                       the view size (2: <= 128, 4: <= 64) */
+    int32_t lsap_wave_max_cols;     /* 0 default (1024); -1 never the one-wave
+                                       kernel; else a long-side limit <= 1024 */
+    int32_t lsap_multi_g;           /* 0 default (auto: as many co-resident
+                                       workgroups per problem as fit, <= 16);
+                                       -1 off; 2..16 forced */
+    int32_t lsap_lds_max_cols;      /* 0 default (4096); -1 off: column state in LDS
+                                       for long sides up to this */
+    int32_t lsap_lds_small_cols;    /* 0 default (2048): ... of which up to this
+                                       with 256 threads (1024 above) */
+    int32_t lsap_mid_max_cols;      /* 0 default (8192): workspace-state long sides
+                                       up to this with 256 threads (1024 above) */
+} mvm_options;
+
+/* Fill *opts with the defaults (all 0) and opts->size. */
+void mvm_options_init(mvm_options *opts);
 
 /*
  * Pairwise symmetric epipolar residuals + per-row argmin, batched over
@@ -82,6 +137,14 @@ int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_
                                  int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
                                  const int64_t *row_offs_dev, float *dist_dev,
                                  int32_t *argmin_dev, float *minval_dev, mvm_stream_t stream);
+/* ... with explicit kernel-path options (NULL = defaults). */
+int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
+                                    const double *F_dev, const int32_t *pair_a,
+                                    const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                    int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
+                                    const int64_t *row_offs_dev, float *dist_dev,
+                                    int32_t *argmin_dev, float *minval_dev,
+                                    const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * Same residuals kept in float64 (no cast), written with a uniform layout:
@@ -114,6 +177,13 @@ int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
                             const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                             float *cube_dev, int32_t *argmin_dev, float *minval_dev,
                             void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream);
+/* ... with explicit kernel-path options (NULL = defaults). */
+int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
+                               const double *F_dev, int32_t n_scenes, int32_t max_n,
+                               const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                               float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                               void *workspace_dev, size_t workspace_bytes,
+                               const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * Batched rectangular linear-sum assignment, identical to
@@ -147,6 +217,20 @@ int mvm_lsap_solve_bounded(const float *cost_dev, const int64_t *cost_offs_dev,
                            void *workspace_dev, size_t workspace_bytes, int64_t *row_ind_dev,
                            int64_t *col_ind_dev, int32_t *status_dev, int64_t long_min,
                            int64_t long_max, mvm_stream_t stream);
+/*
+ * Cost matrices of element type cost_dtype (MVM_F32 or MVM_F64: scipy
+ * assigns a float64 matrix in float64, so a float64 caller must not be
+ * narrowed), with explicit kernel-path options (NULL = defaults).  The
+ * workspace must come from mvm_lsap_plan_ex with the same cost_dtype.
+ */
+int64_t mvm_lsap_plan_ex(int32_t n_problems, const int64_t *rows, const int64_t *cols,
+                         int32_t cost_dtype, int64_t *ws_offs, int64_t *out_offs);
+int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *cost_offs_dev,
+                      const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                      const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                      int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                      int64_t long_min, int64_t long_max, const mvm_options *opts,
+                      mvm_stream_t stream);
 
 /*
  * On-device detection packing, replacing the per-box loop of
@@ -208,8 +292,8 @@ int mvm_select_triangulate(const float *cube_dev, const int64_t *cube_offs_dev,
  * with the fastest 16-byte nontemporal store stream measured on MI355X: 8 KiB
  * per workgroup, workgroups remapped so each XCD writes its own contiguous
  * eighth in order.  bench.py times it to report the achievable HBM write
- * bandwidth next to the kernels' roofline fraction (MVM_PROBE_MODE selects
- * the other patterns studied in DESIGN.md §3.5).
+ * bandwidth next to the kernels' roofline fraction (the other store patterns
+ * studied in DESIGN.md §3.5 live in tools/probes/write_probes.hip).
  */
 int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream);
 

@@ -115,3 +115,48 @@ def test_triangulate_dlt_validation(lib):
     assert lib.mvm_triangulate_dlt(FAKE, None, FAKE, 5, 9, FAKE, None) == 1      # > MVM_MAX_CAMS
     assert b"n_views" in lib.mvm_last_error_string()
     assert lib.mvm_triangulate_dlt(None, None, FAKE, 5, 3, FAKE, None) == 1
+
+
+def test_library_reads_no_environment():
+    """The ABI has no hidden global state: kernel-path choices come only from
+    mvm_options (include/mvmatch.h), so the library imports no getenv."""
+    with open(_native.LIB_PATH, "rb") as fh:
+        blob = fh.read()
+    assert b"getenv\x00" not in blob      # no imported getenv / secure_getenv symbol name
+
+
+def test_options_init_and_validation(lib):
+    o = _native.MvmOptions()
+    lib.mvm_options_init(ctypes.byref(o))
+    assert o.size == ctypes.sizeof(_native.MvmOptions)
+    assert all(getattr(o, n) == 0 for n in _native.OPTION_FIELDS)
+    pa, pb = _pairs((0, 1))
+    bad = _native.make_options(pairwise_rows_per_wave=5)
+    st = lib.mvm_pairwise_residual_argmin_ex(FAKE, FAKE, FAKE, pa, pb, 1, 2, 1, 4, FAKE, FAKE,
+                                             FAKE, FAKE, FAKE, ctypes.byref(bad), None)
+    assert st == 1 and b"rows_per_wave" in lib.mvm_last_error_string()
+    bad = _native.make_options(cube_kernel=9)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(bad), None)
+    assert st == 1 and b"cube_kernel" in lib.mvm_last_error_string()
+    o.size = 3                                      # not a struct size
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(o), None)
+    assert st == 1 and b"size" in lib.mvm_last_error_string()
+    with pytest.raises(ValueError):
+        _native.make_options(no_such_field=1)
+
+
+def test_lsap_plan_dtype(lib):
+    import numpy as np
+    rows, cols = np.array([300, 4], np.int64), np.array([20, 9], np.int64)
+    w32, w64 = np.zeros(3, np.int64), np.zeros(3, np.int64)
+    o = np.zeros(3, np.int64)
+    t32 = lib.mvm_lsap_plan_ex(2, rows.ctypes.data, cols.ctypes.data, _native.MVM_F32,
+                               w32.ctypes.data, o.ctypes.data)
+    t64 = lib.mvm_lsap_plan_ex(2, rows.ctypes.data, cols.ctypes.data, _native.MVM_F64,
+                               w64.ctypes.data, o.ctypes.data)
+    # the tall 300 x 20 problem keeps a transposed copy of its costs: 4 more bytes each
+    assert t64 - t32 >= 300 * 20 * 4
+    assert lib.mvm_lsap_plan_ex(2, rows.ctypes.data, cols.ctypes.data, 7, w32.ctypes.data,
+                                o.ctypes.data) == -1

@@ -14,30 +14,31 @@ def _bits(a):
     return np.asarray(a, dtype=np.float32).view(np.int32)
 
 
-def run_pairwise(dev, pts, cam_offs, F, pairs, S, C, want_dist=True):
+def run_pairwise(dev, pts, cam_offs, F, pairs, S, C, want_dist=True, options=None):
     from bpc_baseline_amd import ops
     plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=dev)
     d, a, m = ops.pairwise_residual_argmin(
         torch.from_numpy(np.ascontiguousarray(pts, np.float64)).to(dev),
         torch.from_numpy(np.ascontiguousarray(cam_offs, np.int64)).to(dev),
-        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan, want_dist=want_dist)
+        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan, want_dist=want_dist,
+        options=options)
     torch.cuda.synchronize()
     return d.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
 
 
-def run_cube(dev, pts, cam_offs, F, S):
+def run_cube(dev, pts, cam_offs, F, S, options=None):
     from bpc_baseline_amd import ops
     plan = ops.TripletPlan(cam_offs, S, device=dev)
     c, a, m = ops.triplet_cost_argmin(
         torch.from_numpy(np.ascontiguousarray(pts, np.float64)).to(dev),
         torch.from_numpy(np.ascontiguousarray(cam_offs, np.int64)).to(dev),
-        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan)
+        torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan, options=options)
     torch.cuda.synchronize()
     return c.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
 
 
-def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
-    d, a, m = run_pairwise(dev, pts, cam_offs, F, pairs, S, C)
+def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C, options=None):
+    d, a, m = run_pairwise(dev, pts, cam_offs, F, pairs, S, C, options=options)
     rd, ra, rm, _, _ = O.pairwise(pts, cam_offs, F, pairs, S, C)
     assert d.shape == rd.shape
     bad = np.nonzero(_bits(d) != _bits(rd))[0]
@@ -47,14 +48,17 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C):
 
 
 # ----------------------------------------------------------- pairwise ----
-@pytest.fixture(params=["lazy_t", "lazy", "eager"])
-def argmin_path(request, monkeypatch):
-    """Run a pairwise test through every argmin path: the lazy one (clean row
+@pytest.fixture(params=["default", "lazy_rows", "eager", "rpw8_rg2", "rpw4"])
+def argmin_path(request):
+    """mvm_options of a pairwise kernel path: the lazy argmin (clean row
     groups: per-chunk minimum, column recovered per group) with its transposed
-    LDS reduction (the default) and with per-row DPP reductions, and the
-    eager one."""
-    monkeypatch.setenv("MVM_PAIRWISE_LAZY", {"lazy_t": "2", "lazy": "1", "eager": "0"}[request.param])
-    return request.param
+    LDS reduction (the default) and with per-row DPP reductions, the eager
+    argmin, and other row-group shapes (8 rows per wave x 2 groups, 4 rows
+    per wave)."""
+    return {"default": {}, "lazy_rows": {"pairwise_argmin": "lazy_rows"},
+            "eager": {"pairwise_argmin": "eager"},
+            "rpw8_rg2": {"pairwise_rows_per_wave": 8, "pairwise_row_groups": 2},
+            "rpw4": {"pairwise_rows_per_wave": 4}}[request.param]
 
 
 @pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),
@@ -63,7 +67,7 @@ def argmin_path(request, monkeypatch):
 def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged, argmin_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, C, n, seed=100 + S * n, ragged=ragged)
-    assert_pairwise_equal(cuda, b.pts, b.cam_offs, b.F, b.pairs, S, C)
+    assert_pairwise_equal(cuda, b.pts, b.cam_offs, b.F, b.pairs, S, C, options=argmin_path)
 
 
 def test_pairwise_golden_4cam(cuda, golden):
@@ -102,7 +106,7 @@ def test_pairwise_f64_kats(cuda, golden):
                           f"{got[bad[:3]]} vs {g['e'][bad[:3]]}"
 
 
-def test_pairwise_edge_cases(cuda):
+def test_pairwise_edge_cases(cuda, argmin_path):
     """Degenerate lines (9999 sentinel), NaN / inf / huge centroids, tails, misalignment."""
     rng = np.random.default_rng(5)
     C, S = 3, 6
@@ -121,7 +125,7 @@ def test_pairwise_edge_cases(cuda):
     F[2] = 0.0                  # both
     F[5] *= 1e-9                # norms near the 1e-8 threshold
     F[7, 2] = 1e70              # huge l2
-    assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C)
+    assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C, options=argmin_path)
 
 
 def test_pairwise_ties_and_duplicates(cuda, argmin_path):
@@ -134,7 +138,7 @@ def test_pairwise_ties_and_duplicates(cuda, argmin_path):
     pts[o + 300] = pts[o + 3]
     pts[o + 517] = pts[o + 3]
     pts[o + 4] = pts[o + 3]
-    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3)
+    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3, options=argmin_path)
 
 
 @pytest.mark.parametrize("n", [256, 512, 1024])
@@ -154,36 +158,42 @@ def test_pairwise_row_minimum_ties(cuda, n, argmin_path):
         ob = int(b.cam_offs[s_ * 3 + cam_b])
         for j in {j0 ^ 1, j0 ^ 3, (j0 + 256) % n, (j0 + 4 * 7 + 1) % n, (j0 + 300) % n}:
             pts[ob + j] = pts[ob + j0]
-    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3)
+    assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3, options=argmin_path)
 
 
 def test_pairwise_argmin_only(cuda, argmin_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(2, 4, 200, seed=9)
-    d, a, m = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False)
+    d, a, m = run_pairwise(cuda, b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False,
+                           options=argmin_path)
     _, ra, rm, _, _ = O.pairwise(b.pts, b.cam_offs, b.F, b.pairs, 2, 4, want_dist=False)
     assert d.size == 0
     assert np.array_equal(a, ra) and np.array_equal(_bits(m), _bits(rm))
 
 
 # --------------------------------------------------------------- cube ----
-@pytest.fixture(params=["small", "fused", "tiled"])
-def cube_path(request, monkeypatch):
-    """Run a cube test through each cube kernel: the small-scene kernel (views
-    of <= 64 detections), the fused tiled kernel (pair residuals computed in
-    the prologue; default up to 256, then its k-chunked form) and the tiled
-    kernel + fp64 workspace (beyond 256: the generic kernel)."""
-    monkeypatch.setenv("MVM_TRIPLET_SMALL", "1" if request.param == "small" else "0")
-    monkeypatch.setenv("MVM_TRIPLET_FUSED", "0" if request.param == "tiled" else "1")
-    monkeypatch.setenv("MVM_TRIPLET_CHUNKED", "0" if request.param == "tiled" else "1")
-    return request.param
+@pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "workspace",
+                        "generic"])
+def cube_path(request):
+    """mvm_options of each cube kernel: the small-scene kernel (views of < 64
+    detections), the fused tiled kernel (pair residuals computed in the
+    prologue; up to 256, then its k-chunked form) with four / two / one
+    (i, j) rows per wave instruction, the tiled kernel over the fp64
+    workspace (beyond 256: the generic kernel) and the generic kernel."""
+    return request.param, {"default": {}, "small": {"cube_kernel": "small"},
+                           "fused": {"cube_kernel": "fused"},
+                           "fused_rows2": {"cube_kernel": "fused", "cube_rows_per_instr": 2},
+                           "fused_rows1": {"cube_kernel": "fused", "cube_rows_per_instr": 1},
+                           "workspace": {"cube_kernel": "workspace"},
+                           "generic": {"cube_kernel": "generic"}}[request.param]
 
 
 def test_cube_golden_batched(cuda, golden, cube_path):
     """All reference compute_cost_matrix cubes in ONE ragged batched launch."""
     g = golden("a3_cost_cubes.npz")
     names = list(g["names"])
-    if cube_path == "small":      # keep the batch inside the small kernel's range
+    path, opts = cube_path
+    if path == "small":           # keep the batch inside the small kernel's range
         names = [n for n in names if max(len(g[f"{n}_p{v}"]) for v in (1, 2, 3)) <= 64]
         assert len(names) >= 8
     views, Fs = [], []
@@ -192,7 +202,8 @@ def test_cube_golden_batched(cuda, golden, cube_path):
         Fs.append(g[f"{n}_F"])
     cam_offs = np.zeros(len(views) + 1, np.int64)
     np.cumsum([len(v) for v in views], out=cam_offs[1:])
-    c, a, _ = run_cube(cuda, np.concatenate(views), cam_offs, np.concatenate(Fs), len(names))
+    c, a, _ = run_cube(cuda, np.concatenate(views), cam_offs, np.concatenate(Fs), len(names),
+                       options=opts)
     co = ro = 0
     for n in names:
         ref = g[f"{n}_cube"]
@@ -212,7 +223,7 @@ def test_cube_golden_batched(cuda, golden, cube_path):
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
-    c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S)
+    c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S, options=cube_path[1])
     rc, ra, rm, _, _ = O.cube(b.pts, b.cam_offs, b.F, S)
     bad = np.nonzero(_bits(c) != _bits(rc))[0]
     assert bad.size == 0, f"{bad.size} cube mismatches"
@@ -287,7 +298,7 @@ def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
         k0 = int(ra[row])
         for k in {k0 ^ 1, (k0 + 256) % n, (k0 + 260) % n, n - 3}:
             pts[o3 + k] = pts[o3 + k0]
-    c, a, m = run_cube(cuda, pts, b.cam_offs, b.F, 1)
+    c, a, m = run_cube(cuda, pts, b.cam_offs, b.F, 1, options=cube_path[1])
     rc, ra, rm, _, _ = O.cube(pts, b.cam_offs, b.F, 1)
     assert np.array_equal(_bits(c), _bits(rc))
     assert np.array_equal(a, ra)

@@ -9,43 +9,35 @@ from scipy.optimize import linear_sum_assignment as scipy_lsa
 pytestmark = pytest.mark.gpu
 
 
-def _batched(cuda, mats):
+def _batched(cuda, mats, options=None, dtype=np.float32):
     from bpc_baseline_amd import ops
-    plan = ops.LsapPlan([m.shape[0] for m in mats], [m.shape[1] for m in mats], device=cuda)
-    flat = np.concatenate([m.astype(np.float32).reshape(-1) for m in mats] + [np.zeros(1, np.float32)])
+    tdt = torch.float32 if dtype == np.float32 else torch.float64
+    plan = ops.LsapPlan([m.shape[0] for m in mats], [m.shape[1] for m in mats], device=cuda, dtype=tdt)
+    flat = np.concatenate([m.astype(dtype).reshape(-1) for m in mats] + [np.zeros(1, dtype)])
     offs = np.zeros(len(mats), np.int64)
     np.cumsum([m.size for m in mats[:-1]], out=offs[1:]) if len(mats) > 1 else None
     r, c, st = ops.linear_sum_assignment_batched(torch.from_numpy(flat).to(cuda),
-                                                 torch.from_numpy(offs).to(cuda), plan)
+                                                 torch.from_numpy(offs).to(cuda), plan,
+                                                 options=options)
     r, c, st = r.cpu().numpy(), c.cpu().numpy(), st.cpu().numpy()
     o = plan.out_offs_host
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
 @pytest.fixture(params=["default", "lds", "workgroup", "workgroup256", "multi"])
-def lsap_path(request, monkeypatch):
-    """default: long sides <= 1024 one problem per wave, up to 4096 one
-    workgroup with the column state in LDS, larger ones split over co-resident
-    workgroups when the batch leaves room; lds: every problem of <= 4096 in
-    the LDS-state workgroup; workgroup: one 1024-thread workgroup per problem
-    with the state in the workspace; multi: every problem split over 4
-    workgroups."""
-    if request.param == "lds":
-        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
-        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
-    elif request.param == "workgroup":
-        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
-        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
-        monkeypatch.setenv("MVM_LSAP_LDS_MAX_COLS", "0")
-    elif request.param == "workgroup256":
-        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
-        monkeypatch.setenv("MVM_LSAP_MULTI_G", "0")
-        monkeypatch.setenv("MVM_LSAP_LDS_MAX_COLS", "0")
-        monkeypatch.setenv("MVM_LSAP_MID_MAX_COLS", "1000000")
-    elif request.param == "multi":
-        monkeypatch.setenv("MVM_LSAP_WAVE_MAX_COLS", "0")
-        monkeypatch.setenv("MVM_LSAP_MULTI_G", "4")
-    return request.param
+def lsap_path(request):
+    """mvm_options of each assignment kernel class.  default: long sides <=
+    1024 one problem per wave, up to 4096 one workgroup with the column state
+    in LDS, larger ones split over co-resident workgroups when the batch
+    leaves room; lds: every problem of <= 4096 in the LDS-state workgroup;
+    workgroup: one 1024-thread workgroup per problem with the state in the
+    workspace; workgroup256: the same with 256 threads; multi: every problem
+    split over 4 workgroups."""
+    off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1}
+    return {"default": None, "lds": off,
+            "workgroup": dict(off, lsap_lds_max_cols=-1),
+            "workgroup256": dict(off, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
+            "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4}}[request.param]
 
 
 def test_random_shapes_and_ties_batched(cuda, lsap_path):
@@ -63,23 +55,78 @@ def test_random_shapes_and_ties_batched(cuda, lsap_path):
             if trial == 3:
                 c = np.zeros(shape, np.float32)
             mats.append(c)
-    for m, (r, c, st) in zip(mats, _batched(cuda, mats)):
+    for m, (r, c, st) in zip(mats, _batched(cuda, mats, lsap_path)):
         r0, c0 = scipy_lsa(m)
         assert st == 0
         assert np.array_equal(r, r0) and np.array_equal(c, c0), m.shape
 
 
+def test_float64_costs_equal_scipy(cuda, lsap_path):
+    """float64 matrices are assigned in float64 (scipy's own precision):
+    values that collapse when narrowed to float32 -- differences below the
+    float32 ulp, ties only in float32 -- must still give scipy's answer."""
+    rng = np.random.default_rng(7)
+    mats = []
+    for shape in [(5, 5), (40, 9), (9, 40), (300, 20), (1100, 5), (2500, 11), (70, 70), (4097, 3)]:
+        mats.append(10.0 + rng.integers(0, 50, size=shape) * 1e-9)   # all equal in float32
+        mats.append(rng.normal(size=shape) * 1e3)
+    got = _batched(cuda, mats, lsap_path, dtype=np.float64)
+    n_diff32 = 0
+    for m, (r, c, st) in zip(mats, got):
+        r0, c0 = scipy_lsa(m)
+        assert st == 0
+        assert np.array_equal(r, r0) and np.array_equal(c, c0), m.shape
+        r32, c32 = scipy_lsa(m.astype(np.float32))
+        n_diff32 += not (np.array_equal(r32, r0) and np.array_equal(c32, c0))
+    assert n_diff32 > 0   # the float32 narrowing really changes some assignments
+
+
 def test_golden_match_lists(cuda, golden, lsap_path):
+    """The reference's match_objects lists from the flattened golden cubes."""
     from bpc_baseline_amd.inference.epipolar_matching import match_objects
     g = golden("a3_cost_cubes.npz")
-    for n in g["names"]:
-        cube = g[f"{n}_cube"]
+    cubes = [g[f"{n}_cube"] for n in g["names"]]
+    flats = [c.reshape(c.shape[0] * c.shape[1], c.shape[2]) for c in cubes]
+    for n, cube, flat, (r, c, st) in zip(g["names"], cubes, flats, _batched(cuda, flats, lsap_path)):
+        assert st == 0
+        M = cube.shape[1]
         for thr, key in ((30, "match30"), (np.inf, "matchinf")):
-            got = np.asarray(match_objects(cube, thr), np.int64).reshape(-1, 3)
+            got = np.asarray([(ri // M, ri % M, ci) for ri, ci in zip(r, c) if flat[ri, ci] < thr],
+                             np.int64).reshape(-1, 3)
             assert np.array_equal(got, g[f"{n}_{key}"]), (n, thr)
+            if lsap_path is None:   # the drop-in itself
+                ours = np.asarray(match_objects(cube, thr), np.int64).reshape(-1, 3)
+                assert np.array_equal(ours, g[f"{n}_{key}"]), (n, thr)
+
+
+def test_match_objects_float64_cube(cuda):
+    """match_objects on a float64 cube assigns in float64 like the reference's
+    scipy call (epipolar_matching.py:106-107), not on a float32 copy."""
+    from bpc_baseline_amd.inference.epipolar_matching import match_objects
+    rng = np.random.default_rng(3)
+    found = 0
+    for trial in range(10):
+        cube = 5.0 + rng.integers(0, 9, (4, 4, 5)) * 1e-10         # all equal in float32
+        flat = cube.reshape(16, 5)
+        r0, c0 = scipy_lsa(flat)
+        ref = [(r // 4, r % 4, c) for r, c in zip(r0, c0) if flat[r, c] < 30]
+        got = match_objects(cube, 30)
+        assert [tuple(int(x) for x in m) for m in got] == [tuple(int(x) for x in m) for m in ref]
+        r32, _ = scipy_lsa(flat.astype(np.float32))
+        found += not np.array_equal(r32, r0)
+    assert found > 0
 
 
 def test_error_statuses(cuda, lsap_path):
+    for mats, want in (([np.array([[np.nan, 1.0], [0.0, 2.0]])], 1), ([np.array([[-np.inf, 1.0]])], 1),
+                       ([np.array([[np.inf, np.inf], [1.0, 2.0]])], 2)):
+        for dtype in (np.float32, np.float64):
+            assert _batched(cuda, mats, lsap_path, dtype=dtype)[0][2] == want
+    r, c, st = _batched(cuda, [np.array([[np.inf, 1.0], [1.0, np.inf]])], lsap_path)[0]
+    assert st == 0 and list(c) == [1, 0]
+
+
+def test_drop_in_error_messages(cuda):
     from bpc_baseline_amd.inference.epipolar_matching import linear_sum_assignment
     with pytest.raises(ValueError, match="invalid numeric"):
         linear_sum_assignment(np.array([[np.nan, 1.0], [0.0, 2.0]]))
@@ -91,19 +138,18 @@ def test_error_statuses(cuda, lsap_path):
     assert list(c) == [1, 0]
 
 
-@pytest.mark.parametrize("multi_g", ["-1", "0", "16"])
-def test_full_256_cube_equals_scipy(cuda, monkeypatch, multi_g):
-    """Config-2 scale: the (65536 x 256) flattened 256^3 cube of one scene."""
+@pytest.mark.parametrize("multi_g", [0, -1, 16])
+def test_full_256_cube_equals_scipy(cuda, multi_g):
+    """Config-2 scale: the (65536 x 256) flattened 256^3 cube of one scene
+    (auto workgroups per problem, one, sixteen)."""
     from bpc_baseline_amd.synth import make_scenes
-    from bpc_baseline_amd.inference.epipolar_matching import linear_sum_assignment
     from oracle import oracle as O
-    monkeypatch.setenv("MVM_LSAP_MULTI_G", multi_g)
     b = make_scenes(1, 3, 256, seed=42)
     cube, _, _, _, _ = O.cube(b.pts, b.cam_offs, b.F, 1)
     flat = cube.reshape(256 * 256, 256)
     r0, c0 = scipy_lsa(flat)
-    r1, c1 = linear_sum_assignment(flat)
-    assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
+    r1, c1, st = _batched(cuda, [flat], {"lsap_multi_g": multi_g})[0]
+    assert st == 0 and np.array_equal(r0, r1) and np.array_equal(c0, c1)
 
 
 @pytest.mark.parametrize("shapes", [
@@ -117,7 +163,7 @@ def test_bounded_launch_sets_every_status(cuda, shapes, lsap_path):
     problem (empty ones included) still gets its status and assignment."""
     rng = np.random.default_rng(3)
     mats = [rng.normal(size=s).astype(np.float32) for s in shapes]
-    for m, (r, c, st) in zip(mats, _batched(cuda, mats)):
+    for m, (r, c, st) in zip(mats, _batched(cuda, mats, lsap_path)):
         assert st == 0
         if m.size:
             r0, c0 = scipy_lsa(m)

@@ -20,21 +20,19 @@ rows = np.full(b.n_scenes, n * n, np.int64)
 cols = np.full(b.n_scenes, n, np.int64)
 offs = torch.from_numpy(tp.cube_offs_host[:-1].copy()).to(dev)
 
-def gpu_run(k):
+def gpu_run(k, options=None):
     plan = ops.LsapPlan(rows[:k], cols[:k], device=dev)
-    ops.linear_sum_assignment_batched(cube, offs[:k], plan)        # warm
+    ops.linear_sum_assignment_batched(cube, offs[:k], plan, options=options)        # warm
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    r, c, st = ops.linear_sum_assignment_batched(cube, offs[:k], plan)
+    r, c, st = ops.linear_sum_assignment_batched(cube, offs[:k], plan, options=options)
     e1.record()
     torch.cuda.synchronize()
     assert int(st.max()) == 0
     return e0.elapsed_time(e1) * 1e-3, r.cpu().numpy(), c.cpu().numpy()
 
-os.environ["MVM_LSAP_MULTI_G"] = "0"
-t1w, _, _ = gpu_run(1)
-os.environ.pop("MVM_LSAP_MULTI_G")
+t1w, _, _ = gpu_run(1, {"lsap_multi_g": -1})   # one workgroup per problem
 t1, r1, c1 = gpu_run(1)
 host0 = cube[: n * n * n].cpu().numpy().reshape(n * n, n)
 ts = time.perf_counter(); r0, c0 = scipy_lsa(host0); ts = time.perf_counter() - ts

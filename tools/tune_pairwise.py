@@ -1,7 +1,10 @@
-"""Interleaved A/B of pairwise-kernel variants in ONE process (rule: perf deltas
-from interleaved rounds).  Variants are selected with the MVM_PAIRWISE_RPW knob.
+"""Interleaved A/B of pairwise-kernel paths in ONE process (perf deltas from
+interleaved rounds), selected with explicit mvm_options.  Every variant's
+association and first matrix bytes must equal the first variant's.
 
-python tools/tune_pairwise.py [--scenes 1000] [--rounds 5] [--variants 4,8,16]
+python tools/tune_pairwise.py [--scenes 1000] [--cams 4] [--dets 1024] [--rounds 5]
+                              [--variants default,eager,rpw8]
+Variants: a name below, or RPW[:RG[:ARGMIN]] (e.g. 16:4:lazy_rows).
 """
 import argparse
 import os
@@ -14,14 +17,31 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bpc_baseline_amd import ops  # noqa: E402
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
+NAMED = {"default": {}, "eager": {"pairwise_argmin": "eager"},
+         "lazy_rows": {"pairwise_argmin": "lazy_rows"},
+         "rpw8": {"pairwise_rows_per_wave": 8}, "rpw4": {"pairwise_rows_per_wave": 4}}
+
+
+def options_of(v: str) -> dict:
+    if v in NAMED:
+        return NAMED[v]
+    rpw, _, rest = v.partition(":")
+    rg, _, argmin = rest.partition(":")
+    o = {"pairwise_rows_per_wave": int(rpw)}
+    if rg:
+        o["pairwise_row_groups"] = int(rg)
+    if argmin:
+        o["pairwise_argmin"] = argmin
+    return o
+
+
 ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=1000)
 ap.add_argument("--cams", type=int, default=4)
 ap.add_argument("--dets", type=int, default=1024)
 ap.add_argument("--rounds", type=int, default=5)
-ap.add_argument("--variants", default="4,8,16", help="RPW or RPW:RG[:LANE_RESULTS[:NT[:XCD[:INTERLEAVE[:STAGGER[:LAZY[:LDS_PAD]]]]]]] list")
-ap.add_argument("--no-dist", action="store_true")
-ap.add_argument("--no-argmin", action="store_true", help="distances only (argmin template off)")
+ap.add_argument("--variants", default="default")
+ap.add_argument("--no-dist", action="store_true", help="association only (no matrix output)")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -31,39 +51,21 @@ pts = torch.from_numpy(b.pts).to(dev)
 co = torch.from_numpy(b.cam_offs).to(dev)
 F = torch.from_numpy(b.F).to(dev)
 dist = torch.empty(0 if args.no_dist else plan.n_dist, dtype=torch.float32, device=dev)
-am = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.int32, device=dev)
-mv = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.float32, device=dev)
-nbytes = 16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0] + (0 if args.no_dist else 4.0 * plan.n_dist) + 8.0 * plan.n_rows
+am = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
+mv = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
+nbytes = (16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0] + (0 if args.no_dist else 4.0 * plan.n_dist)
+          + 8.0 * plan.n_rows)
 variants = [v.strip() for v in args.variants.split(",")]
 times = {v: [] for v in variants}
 ref = None
 for rnd in range(args.rounds + 1):
     for v in variants:
-        rpw, _, rg = v.partition(":")
-        rg, _, lr = rg.partition(":")
-        lr, _, nt = lr.partition(":")
-        nt, _, xcd = nt.partition(":")
-        xcd, _, ilv = xcd.partition(":")
-        ilv, _, stg = ilv.partition(":")
-        stg, _, lazy = stg.partition(":")
-        lazy, _, pad = lazy.partition(":")
-        os.environ["MVM_PAIRWISE_LDS_PAD"] = pad or "0"
-        os.environ["MVM_PAIRWISE_STAGGER"] = stg or "0"
-        os.environ["MVM_PAIRWISE_LAZY"] = lazy or "2"
-        os.environ["MVM_PAIRWISE_INTERLEAVE"] = ilv or "0"
-        os.environ["MVM_PAIRWISE_LANE_RESULTS"] = lr or "1"
-        os.environ["MVM_PAIRWISE_NT"] = nt or "1"
-        os.environ["MVM_PAIRWISE_XCD"] = xcd or "0"
-        os.environ["MVM_PAIRWISE_RPW"] = rpw
-        if rg:
-            os.environ["MVM_PAIRWISE_RG"] = rg
-        else:
-            os.environ.pop("MVM_PAIRWISE_RG", None)
+        opt = options_of(v)
+        ops.pairwise_residual_argmin(pts, co, F, plan, out=(dist, am, mv), options=opt)   # warm
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ops.pairwise_residual_argmin(pts, co, F, plan, out=(dist, am, mv))   # warm this variant
         e0.record()
         for _ in range(3):
-            ops.pairwise_residual_argmin(pts, co, F, plan, out=(dist, am, mv))
+            ops.pairwise_residual_argmin(pts, co, F, plan, out=(dist, am, mv), options=opt)
         e1.record()
         torch.cuda.synchronize()
         if rnd > 0:
@@ -74,6 +76,6 @@ for rnd in range(args.rounds + 1):
         assert chk == ref, f"variant {v} differs"
 for v in variants:
     t = np.array(times[v])
-    print(f"RPW:RG={v:>5}: median {np.median(t):.3f} ms  min {t.min():.3f} ms  "
+    print(f"{v:>12}: median {np.median(t):.3f} ms  min {t.min():.3f} ms  "
           f"{nbytes / (np.median(t) * 1e-3) / 1e9:.0f} GB/s  "
           f"{plan.n_dist / (np.median(t) * 1e-3):.3e} pairs/s")
