@@ -612,6 +612,65 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
             }
         }
     };
+    // Full tiles (every lane's 4 k inside the view, all 8 wave rows present:
+    // the whole 256^3 regime): the fast loop without per-row existence tests
+    // or exec masking, rows stored from one running scalar address, and the
+    // in-lane argmin from unsigned minima of the float32 bits (the values are
+    // finite and non-negative here, so they order like their bits) -- the
+    // first q holding the minimum is np.argmin's first index within the lane.
+    auto full_loop = [&]() {
+        constexpr uint64_t kRowBytes = kChunk * sizeof(float);
+        uint64_t rp = reinterpret_cast<uint64_t>(args.cube + coff) +
+                      (uint64_t)((int64_t)i0 * M + j0) * kRowBytes;
+        const uint64_t i_step = (uint64_t)M * kRowBytes;
+        for (int ii = 0; ii < ni; ++ii) {
+            double a13[kColsPerLane];
+            {
+                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+            }
+            uint32_t key[kCubeRPW];
+            int32_t idx[kCubeRPW];
+            uint64_t p = rp;
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; ++r) {
+                const double v12 = s12[ii][wave * kCubeRPW + r];
+                float v[kColsPerLane];
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q)
+                    v[q] = (float)third_q((v12 + a13[q]) + a23[r][q]);   // (e12 + e13) + e23, :81
+                uint32_t off = (uint32_t)kb * 4u;
+                __asm__ volatile("" : "+v"(off));   // a 32-bit lane offset at the store: saddr form
+                store4_nt_row(p, off, v);
+                p += kRowBytes;
+                __asm__ volatile("" : "+s"(p));     // one running scalar row address
+                const uint32_t b0 = __float_as_uint(v[0]), b1 = __float_as_uint(v[1]);
+                const uint32_t b2 = __float_as_uint(v[2]), b3 = __float_as_uint(v[3]);
+                const uint32_t m = umin(min3_u32(b0, b1, b2), b3);
+                int q = (b2 == m) ? 2 : 3;
+                q = (b1 == m) ? 1 : q;
+                q = (b0 == m) ? 0 : q;
+                key[r] = m;                       // the bits themselves: no NaN / invalid here
+                idx[r] = kb + q;
+            }
+            uint32_t mk;
+            int32_t mi;
+            wave_argmin8_transposed(key, idx, lane, mk, mi);
+            if (lane < kCubeRPW) {
+                const int64_t row = roff + (int64_t)(i0 + ii) * M + j0 + lane;
+                if (args.argmin) args.argmin[row] = mi;
+                if (args.minval) args.minval[row] = __uint_as_float(mk);
+            }
+            rp += i_step;
+        }
+    };
+    if constexpr (SPLIT == 1) {
+        if (tile_fast && nrows == kCubeRPW && P == kChunk) {   // uniform
+            full_loop();
+            return;
+        }
+    }
     if (tile_fast) main_loop(std::integral_constant<bool, true>{});
     else main_loop(std::integral_constant<bool, false>{});
 }

@@ -193,6 +193,11 @@ __device__ __forceinline__ uint32_t dpp_from(uint32_t v) {
 
 __device__ __forceinline__ uint32_t umin(uint32_t a, uint32_t b) { return a < b ? a : b; }
 
+__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
+    const uint32_t ab = a < b ? a : b;   // -> v_min3_u32
+    return ab < c ? ab : c;
+}
+
 // Argmin of 8 rows over the wave when every lane's column indices exceed
 // those of the lanes below it (one k-chunk of the cube: lane l holds columns
 // 4l..4l+3, idx = its first minimum).  A transposing butterfly reduces the 8

@@ -138,10 +138,6 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
 // chunk, `lazy_recover`), so the result is exactly np.argmin's: the earliest
 // chunk wins inside a lane (strict '<'), the lowest q inside a chunk, and
 // rows whose minimum sits in several lanes take the tie path.
-__device__ __forceinline__ uint32_t min3_u32(uint32_t a, uint32_t b, uint32_t c) {
-    const uint32_t ab = a < b ? a : b;   // -> v_min3_u32
-    return ab < c ? ab : c;
-}
 
 // float32 bits of the 4 stored values of one lane for one row (row_fast's arithmetic)
 __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double rl1, double rl2,
