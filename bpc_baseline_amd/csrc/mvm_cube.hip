@@ -630,12 +630,19 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                 const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
                 a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
             }
+            double v12s[kCubeRPW];   // the 8 rows' e12, read together (4 x 16 B)
+#pragma unroll
+            for (int r = 0; r < kCubeRPW; r += 2) {
+                const f64x2 w = *reinterpret_cast<const f64x2 *>(&s12[ii][wave * kCubeRPW + r]);
+                v12s[r] = w.x;
+                v12s[r + 1] = w.y;
+            }
             uint32_t key[kCubeRPW];
             int32_t idx[kCubeRPW];
             uint64_t p = rp;
 #pragma unroll
             for (int r = 0; r < kCubeRPW; ++r) {
-                const double v12 = s12[ii][wave * kCubeRPW + r];
+                const double v12 = v12s[r];
                 float v[kColsPerLane];
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q)

@@ -28,6 +28,7 @@ from typing import List, Sequence, Tuple
 import numpy as np
 import torch
 from .. import ops
+from .capture_session import cube_slot, lsap_slot
 
 __all__ = [
     "epipolar_error", "epipolar_error_full", "compute_cost_matrix", "match_objects",
@@ -130,8 +131,8 @@ def compute_cost_matrix(dets1, dets2, dets3, F12, F13, F23, img1=None, img2=None
     N, M, P = (len(v) for v in views)
     if N == 0 or M == 0 or P == 0:
         return np.zeros((N, M, P), dtype=np.float32)     # the reference loop never runs
-    cubes, _ = compute_cost_matrices([views], [(F12, F13, F23)])
-    return cubes[0]
+    # one staged copy in, one launch, one copy out (capture_session)
+    return cube_slot(N, M, P, _device()).run(views, (F12, F13, F23))
 
 
 _LSAP_ERRORS = {1: "matrix contains invalid numeric entries", 2: "cost matrix is infeasible",
@@ -152,14 +153,13 @@ def linear_sum_assignment(cost_matrix):
     if cost.ndim != 2:
         raise ValueError("expected a matrix")
     tdt = torch.float32 if dt == np.float32 else torch.float64
-    plan = ops.LsapPlan([cost.shape[0]], [cost.shape[1]], device=dev, dtype=tdt)
-    cost_d = torch.from_numpy(cost.reshape(-1) if cost.size else np.zeros(1, dt)).to(dev)
-    offs = torch.zeros(1, dtype=torch.int64, device=dev)
-    r, c, st = ops.linear_sum_assignment_batched(cost_d, offs, plan)
-    status = int(st.cpu()[0])
+    if cost.size == 0:                  # scipy: empty assignment
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    # one staged copy in, one launch, one copy out (capture_session)
+    r, c, status = lsap_slot(cost.shape[0], cost.shape[1], tdt, dev).run(cost)
     if status:
         raise ValueError(_LSAP_ERRORS.get(status, f"assignment failed ({status})"))
-    return r.cpu().numpy(), c.cpu().numpy()
+    return r, c
 
 
 def match_objects(cost_matrix, threshold) -> List[Tuple[int, int, int]]:

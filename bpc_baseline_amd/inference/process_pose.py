@@ -34,6 +34,7 @@ import numpy as np
 import torch
 
 from .. import ops
+from .capture_session import cube_slot
 from .epipolar_matching import _device, compute_cost_matrix, match_objects, triangulate_multi_view
 from .utils.camera_utils import compute_fundamental_matrix
 
@@ -122,15 +123,11 @@ def detect_capture(yolo, capture, conf_thresh: float, *, imgsz: int = 1280,
 
 
 def _packed_cube(det: PackedDetections, F12, F13, F23) -> np.ndarray:
-    """The cost cube straight from the packed device centroids of images 0-2."""
-    dev = det.pts.device
-    off3 = det.cam_offs_host[:4]
-    plan = ops.TripletPlan(off3, 1, device=dev)
-    F = torch.from_numpy(np.stack([np.asarray(f, np.float64).reshape(9) for f in (F12, F13, F23)])
-                         .reshape(-1)).to(dev)
-    cam_offs = det.cam_offs[:4].contiguous()
-    cube, _, _ = ops.triplet_cost_argmin(det.pts, cam_offs, F, plan)
-    return cube.cpu().numpy().reshape(*(int(c) for c in np.diff(off3)))
+    """The cost cube straight from the packed device centroids of images 0-2
+    (only F travels host -> device; capture_session's cached slot)."""
+    N, M, P = (int(c) for c in np.diff(det.cam_offs_host[:4]))
+    slot = cube_slot(N, M, P, det.pts.device)
+    return slot.run(None, (F12, F13, F23), pts=det.pts, cam_offs=det.cam_offs[:4])
 
 
 def match_detections(capture, detections: Dict[int, list], params=None, *,
@@ -158,15 +155,16 @@ def match_detections(capture, detections: Dict[int, list], params=None, *,
         cost = compute_cost_matrix(d1, d2, d3, F12, F13, F23)
     N, M, P = cost.shape
     # the reference prints stats and samples with the global RNG; keep the
-    # RNG consumption identical even when quiet
+    # RNG consumption identical even when quiet (the text is built only to print)
     lines = ["\n--- Cost Matrix Stats ---", f"Shape: {cost.shape}",
              f"Min: {cost.min():.4f}, Max: {cost.max():.4f}, Mean: {cost.mean():.4f}",
-             "\nRandom samples from cost_matrix:"]
+             "\nRandom samples from cost_matrix:"] if verbose else []
     for _ in range(min(5, N * M * P)):
         i = np.random.randint(0, N)
         j = np.random.randint(0, M)
         k = np.random.randint(0, P)
-        lines.append(f"  cost_matrix[{i},{j},{k}] = {cost[i, j, k]:.4f}")
+        if verbose:
+            lines.append(f"  cost_matrix[{i},{j},{k}] = {cost[i, j, k]:.4f}")
     if verbose:
         print("\n".join(lines))
 

@@ -147,8 +147,9 @@ def make_scenes(n_scenes: int, n_cams: int, n_dets, *, seed: int = 0, first_scen
                 ragged: bool = False, pairs: Optional[np.ndarray] = None) -> SceneBatch:
     """Scenes ``first_scene .. first_scene + n_scenes - 1`` of the seeded family.
 
+    ``n_dets`` is one count for every view or a per-camera list;
     ``ragged=True`` draws each view's count uniformly from [0, n_dets] (empty
-    views included) instead of using ``n_dets`` for every view.
+    views included) instead.
     """
     if pairs is None:
         pairs = camera_pairs(n_cams)
@@ -158,7 +159,10 @@ def make_scenes(n_scenes: int, n_cams: int, n_dets, *, seed: int = 0, first_scen
     RT_all = np.empty((n_scenes, n_cams, 4, 4), dtype=np.float64)
     for s in range(n_scenes):
         rng = np.random.default_rng(seed + first_scene + s)
-        per_view = rng.integers(0, int(n_dets) + 1, size=n_cams) if ragged else [int(n_dets)] * n_cams
+        if ragged:
+            per_view = rng.integers(0, int(n_dets) + 1, size=n_cams)
+        else:
+            per_view = [int(n_dets)] * n_cams if np.isscalar(n_dets) else [int(x) for x in n_dets]
         Ks, RTs = make_rig(rng, n_cams)
         K_all[s], RT_all[s] = np.stack(Ks), np.stack(RTs)
         for c, (_, cxy) in enumerate(_views(rng, Ks, RTs, list(per_view), box_px=80.0, noise_px=1.5)):

@@ -308,3 +308,31 @@ def test_detect_then_match_dropin(cuda, golden):
             np.testing.assert_array_equal(p.boxes, z[f"m{c}_boxes"][q])
             np.testing.assert_array_equal(p.centroids, z[f"m{c}_centroids"][q])
             np.testing.assert_allclose(p.t, z[f"m{c}_t"][q], rtol=1e-12, atol=1e-9)
+
+
+def test_cached_slots_across_shapes_and_repeats(cuda):
+    """compute_cost_matrix / match_objects reuse per-shape launch state
+    (inference/capture_session.py): interleaved shapes, repeats of a shape,
+    and float64 cubes must give exactly the oracle cube and scipy's matches
+    on every call, and each returned cube is a fresh array."""
+    from scipy.optimize import linear_sum_assignment as scipy_lsa
+    from bpc_baseline_amd.inference.epipolar_matching import compute_cost_matrix, match_objects
+    from bpc_baseline_amd.synth import make_scenes
+    seen = []
+    for it, n in enumerate([2, 4, 2, (4, 3, 5), 4, 24, 2, (40, 7, 9), 24, (4, 3, 5)]):
+        counts = (n, n, n) if np.isscalar(n) else n
+        b = make_scenes(1, 3, list(counts), seed=50 + it)
+        views = [b.pts[b.cam_offs[c]:b.cam_offs[c + 1]] for c in range(3)]
+        F = b.F.reshape(3, 3, 3)
+        cube = compute_cost_matrix(_dets(views[0]), _dets(views[1]), _dets(views[2]), F[0], F[1], F[2])
+        ref = O.cube(b.pts, b.cam_offs, b.F, 1)[0].reshape(counts)
+        assert np.array_equal(_b32(cube), _b32(ref)), (it, counts)
+        assert all(cube is not s and not np.shares_memory(cube, s) for s in seen)
+        seen.append(cube)
+        for c in (cube, cube.astype(np.float64) * 1.5):
+            N, M, P = c.shape
+            flat = c.reshape(N * M, P)
+            r0, c0 = scipy_lsa(flat)
+            want = [(r // M, r % M, k) for r, k in zip(r0, c0) if flat[r, k] < 30]
+            got = [tuple(int(x) for x in m) for m in match_objects(c, 30)]
+            assert got == [tuple(int(x) for x in m) for m in want], (it, c.dtype)
