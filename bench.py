@@ -359,9 +359,11 @@ def main():
     torch.cuda.synchronize(dev)
     env.barrier()
 
-    # ---- one hipGraph per step (single GPU): the launches replay back to back
-    # without the per-call host path (op dispatch, argument checks), which is
-    # longer than a C2 kernel.  The same kernels run on the same data each step.
+    # ---- single GPU: the K timed steps as ONE hipGraph (captured once,
+    # outside the timed region), so the launches of consecutive steps run back
+    # to back without the per-call host path (op dispatch, argument checks)
+    # and without a graph launch per step (~30 us, longer than a fifth of a C2
+    # kernel).  Every step still runs every launch over its whole batch.
     graph = None
     if args.graph == "on" or (args.graph == "auto" and not env.initialised):
         if env.initialised:
@@ -369,17 +371,15 @@ def main():
                              "(the step's gather is a collective)")
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            for c in chunks:
-                launch(c)
+            for _ in range(args.steps):
+                for c in chunks:
+                    launch(c)
         graph.replay()
         torch.cuda.synchronize(dev)
         step_bytes = sum(c.nbytes for c in chunks)
 
-        def step(events=None):  # noqa: F811 -- the graph form of the step
-            graph.replay()      # timed by one event pair around all the steps (below)
-            return None
-
     events = []
+    gathered = None
     torch.cuda.synchronize(dev)
     env.barrier()
     with ClockSampler() as clocks:
@@ -387,12 +387,13 @@ def main():
         if graph is not None:   # one event pair over the timed region: no markers between steps
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record(stream)
-        for _ in range(args.steps):
-            gathered = step(events)
-        if graph is not None:
+            graph.replay()      # the K steps
             ev1.record(stream)
             events.append((ev0, ev1, step_bytes * args.steps, units_local * args.steps,
                            len(chunks) * args.steps))
+        else:
+            for _ in range(args.steps):
+                gathered = step(events)
         torch.cuda.synchronize(dev)
         env.barrier()
         elapsed = time.perf_counter() - t_start
@@ -554,8 +555,8 @@ def main():
             "n_scenes_total": n_local * world if args.scaling == "weak" else wl["n_scenes"],
             "scenes_per_launch": chunk, "launches_per_step": len(chunks),
             "units_per_gpu_step": units_local,
-            "launch": ("one hipGraph replay per step (captured once, outside the timed region)"
-                       if graph is not None else "eager op calls"),
+            "launch": ("one hipGraph holding the K steps' launches, captured once outside the "
+                       "timed region, replayed once" if graph is not None else "eager op calls"),
             "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
                             f"({env.backend}{', overlapped per launch' if overlap else ''})")
                            if env.initialised else "single GPU",
@@ -579,8 +580,8 @@ def main():
             "traffic": (traffic or {}).get("bytes_per_launch"),
             "bytes_per_launch": float(byts.sum() / n_launch),
             "avg_launch_ms": avg_dur * 1e3,
-            "event_scope": ("one event pair over the timed region: includes the dispatch gap "
-                            "between graph replays" if graph is not None else
+            "event_scope": ("one event pair over the timed region (one graph replay of the K "
+                            "steps): includes the gaps between kernel nodes" if graph is not None else
                             "one event pair per launch"),
             "units_per_s_in_kernel": float(units_ev.sum() / durs.sum()),
             "write_probe_gbs": probe_gbs,

@@ -629,6 +629,7 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;    // default: 64 rows per row group
 constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
+constexpr int64_t kMinBlocks = 4096; // ~8 rounds of 2 resident workgroups on 256 CUs
 
 int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
                int n_cams) {
@@ -706,12 +707,21 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
                         (int)o.pairwise_row_groups);
-    // default: enough row groups to amortise the column lines over >= ~256
-    // rows, but never more than the rows a view has
+    // default: enough row groups to amortise the column lines over ~256 rows,
+    // never more than the rows a view has -- halved to ~128 rows while the
+    // grid has fewer than kMinBlocks workgroups: the last round of long-lived
+    // workgroups is a tail with idle CUs (C2, 3,000 matrices of 256 rows:
+    // 0.156 -> 0.143 ms per launch; C3's 24,000 blocks keep 256 rows)
     const int groups_needed = (max_rows + kWaves * rpw - 1) / (kWaves * rpw);
-    const int rg = o.pairwise_row_groups ? o.pairwise_row_groups
-                                         : max(1, min(groups_needed, 256 / (kWaves * rpw)));
     const int64_t sp_count = (int64_t)n_scenes * a.n_pairs;
+    int rg = o.pairwise_row_groups;
+    if (!rg) {
+        rg = max(1, min(groups_needed, 256 / (kWaves * rpw)));
+        const int rg_floor = min(rg, max(1, 128 / (kWaves * rpw)));
+        while (rg > rg_floor &&
+               sp_count * ((max_rows + kWaves * rpw * rg - 1) / (kWaves * rpw * rg)) < kMinBlocks)
+            rg /= 2;
+    }
     const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
     const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
     if (blocks > 0x7FFFFFFFLL)

@@ -171,9 +171,9 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
 @pytest.mark.gpu
 @pytest.mark.parametrize("workload", ["c3", "c2cube"])
 def test_bench_graph_replay_single_gpu(tmp_path, workload):
-    """bench.py's single-GPU step as one hipGraph replay: the captured launches
-    run on every replay (the last launch's outputs are bit-exact vs the oracle)
-    and the per-launch event average covers every launch of the step."""
+    """bench.py's single-GPU timed steps as one hipGraph replay: the captured
+    launches of every step run (the last launch's outputs are bit-exact vs the
+    oracle) and the per-launch event average covers every launch of every step."""
     import json
     import subprocess
     import sys
@@ -187,6 +187,6 @@ def test_bench_graph_replay_single_gpu(tmp_path, workload):
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["parity"].startswith("bit-exact")
-    assert line["config"]["launch"].startswith("one hipGraph replay")
+    assert line["config"]["launch"].startswith("one hipGraph holding the K steps")
     assert line["config"]["launches_per_step"] == 3
     assert line["roofline"]["avg_launch_ms"] > 0
