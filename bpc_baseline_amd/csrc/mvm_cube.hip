@@ -385,7 +385,18 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int t = threadIdx.x;
     const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
     const int lane = t % kWave;
-    const uint32_t blk = blockIdx.x;
+    // Write order.  Dispatch puts workgroup b on XCD b % 8; the remap gives
+    // each XCD a contiguous range of tiles, so one XCD holds all the tiles of
+    // a scene at once.  A tile owns the i rows ib, ib + IB', ib + 2 IB', ...
+    // (IB' = i_blocks: interleaved, not 16 consecutive rows), so at its
+    // step ii the scene's tiles write the ADJACENT rows ii * IB' .. ii * IB' +
+    // IB' - 1 -- one contiguous band of the cube per XCD, moving through it as
+    // ii advances, instead of 16 bands 16 rows apart.
+    uint32_t blk = blockIdx.x;
+    {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
     const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
     const int s = (int)(blk / per_scene);
     const int rem = (int)(blk % per_scene);
@@ -395,9 +406,9 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
     const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
     const int jw0 = jb * kJ;
-    const int i0 = ib * kCubeIB;
-    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
-    const int ni = min(kCubeIB, N - i0);
+    const int i_stride = args.i_blocks;                 // tile rows: ib + i_stride * ii
+    if (jw0 >= M || ib >= N || P == 0) return;          // uniform over the workgroup
+    const int ni = min(kCubeIB, (N - ib + i_stride - 1) / i_stride);
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
     const int hl = lane / kLPR;                                      // row group of the lane
@@ -412,19 +423,31 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
     const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
 
-    // ---- prologue 1: the tile's view-0 rows and view-1 rows/columns --------
+    // ---- prologue 1: the tile's view-0 rows, view-1 rows/columns, and the
+    // k columns' lines (one column per thread: kThreads == kChunk).  The F23
+    // column lines are shared by the 4 waves: they go to the s13 storage as
+    // scratch (read back in prologue 2, before e13 overwrites it) instead of
+    // every wave recomputing them
+    struct ColRec {
+        LineRec l;
+        double x, y;
+    };
+    static_assert(sizeof(ColRec) * kChunk <= sizeof(s13), "F23 column scratch fits s13");
+    ColRec *s_c23 = reinterpret_cast<ColRec *>(&s13[0][0]);
+    bool any_deg = false;   // a degenerate line among this thread's (9999 sentinel)
     if (t < kCubeIB) {
         LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
         double px = 0.0, py = 0.0;
         if (t < ni) {
             double f[9];
-            px = args.pts[2 * (c0 + i0 + t)];
-            py = args.pts[2 * (c0 + i0 + t) + 1];
+            px = args.pts[2 * (c0 + ib + i_stride * t)];
+            py = args.pts[2 * (c0 + ib + i_stride * t) + 1];
             load_f(F13, f);
             a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
             load_f(F12, f);
             b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
         }
+        any_deg |= (a.deg != 0.0) || (b.deg != 0.0);
         s_r13[t] = a;
         s_r12[t] = b;
         s_p0[t][0] = px;
@@ -442,63 +465,75 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
             load_f(F23, f);
             b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
         }
+        any_deg |= (a.deg != 0.0) || (b.deg != 0.0);
         s_c12[jj] = a;
         s_r23[jj] = b;
         s_p1[jj][0] = px;
         s_p1[jj][1] = py;
     }
-    __syncthreads();
-    // ---- prologue 2: the tile's pair residuals (row_safe's arithmetic) -------
-    bool tame_in = true;   // every residual this thread produced is <= kTameResidual
+    LineRec cl13{0.0, 0.0, 0.0, 0.0};   // column k = t, F13 (registers, for e13)
+    double kx = 0.0, ky = 0.0;
     {
-        const int k = t;                                   // kThreads == kChunk: one column each
-        if (k < P) {
+        ColRec c23{{0.0, 0.0, 0.0, 0.0}, 0.0, 0.0};
+        if (t < P) {
             double f[9];
+            kx = args.pts[2 * (c2 + t)];
+            ky = args.pts[2 * (c2 + t) + 1];
             load_f(F13, f);
-            const double x = args.pts[2 * (c2 + k)], y = args.pts[2 * (c2 + k) + 1];
-            LineRec cl{0.0, 0.0, 0.0, 0.0};
-            cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
-#pragma unroll 4
-            for (int r = 0; r < kCubeIB; ++r) {
-                const double e = r < ni ? pair_e(cl, s_r13[r], s_p0[r][0], s_p0[r][1], x, y) : 0.0;
-                s13[r][k] = e;
-                tame_in &= e <= kTameResidual;
-            }
-        } else {
-            for (int r = 0; r < kCubeIB; ++r) s13[r][k] = 0.0;
+            cl13.deg = col_line(f, kx, ky, cl13.l0, cl13.l1, cl13.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            c23.l.deg = col_line(f, kx, ky, c23.l.l0, c23.l.l1, c23.l.l2) ? 1.0 : 0.0;
+            c23.x = kx;
+            c23.y = ky;
+            any_deg |= (cl13.deg != 0.0) || (c23.l.deg != 0.0);
         }
+        s_c23[t] = c23;
+    }
+    // uniform: no line of the tile is degenerate, so every residual is
+    // 0.5 * (|l1 . p1| + |l2 . p2|) without the sentinel selects
+    const bool no_deg = __syncthreads_and(!any_deg) != 0;
+    auto pair = [&](const LineRec &col, const LineRec &row, double rx, double ry, double cx,
+                    double cy) {
+        if (no_deg)
+            return 0.5 * (line_dist(col.l0, col.l1, col.l2, rx, ry) +
+                          line_dist(row.l0, row.l1, row.l2, cx, cy));   // :28
+        return pair_e(col, row, rx, ry, cx, cy);
+    };
+    // ---- prologue 2: the wave's e23 rows into registers ---------------------
+    bool tame_in = true;   // every residual this thread produced is <= kTameResidual
+    double a23[kLaneRows][kColsPerLane];
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const ColRec cl = s_c23[min(kb + q, kChunk - 1)];
+#pragma unroll
+        for (int r = 0; r < kLaneRows; ++r) {
+            const int rr = r + hl * kLaneRows;            // the wave row
+            const int jj = wave * kCubeRPW + rr;
+            a23[r][q] = (rr < nrows && q < kvalid)
+                            ? pair(cl.l, s_r23[jj], s_p1[jj][0], s_p1[jj][1], cl.x, cl.y)
+                            : 0.0;
+            tame_in &= a23[r][q] <= kTameResidual;
+        }
+    }
+    __syncthreads();   // every wave has its F23 columns: s13 is free for e13
+    // ---- prologue 3: the tile's e13 / e12 (row_safe's arithmetic) -----------
+    if (t < P) {
+#pragma unroll 4
+        for (int r = 0; r < kCubeIB; ++r) {
+            const double e = r < ni ? pair(cl13, s_r13[r], s_p0[r][0], s_p0[r][1], kx, ky) : 0.0;
+            s13[r][t] = e;
+            tame_in &= e <= kTameResidual;
+        }
+    } else {
+        for (int r = 0; r < kCubeIB; ++r) s13[r][t] = 0.0;
     }
     for (int x = t; x < kCubeIB * kJ; x += kThreads) {
         const int r = x / kJ, jj = x % kJ;
         const double e = (r < ni && jw0 + jj < M)
-                             ? pair_e(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
+                             ? pair(s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1])
                              : 0.0;
         s12[r][jj] = e;
         tame_in &= e <= kTameResidual;
-    }
-    double a23[kLaneRows][kColsPerLane];
-    {
-        double f[9];
-        load_f(F23, f);
-#pragma unroll
-        for (int q = 0; q < kColsPerLane; ++q) {
-            LineRec cl{0.0, 0.0, 0.0, 0.0};
-            double x = 0.0, y = 0.0;
-            if (q < kvalid) {
-                x = args.pts[2 * (c2 + kb + q)];
-                y = args.pts[2 * (c2 + kb + q) + 1];
-                cl.deg = col_line(f, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
-            }
-#pragma unroll
-            for (int r = 0; r < kLaneRows; ++r) {
-                const int rr = r + hl * kLaneRows;            // the wave row
-                const int jj = wave * kCubeRPW + rr;
-                a23[r][q] = (rr < nrows && q < kvalid)
-                                ? pair_e(cl, s_r23[jj], s_p1[jj][0], s_p1[jj][1], x, y)
-                                : 0.0;
-                tame_in &= a23[r][q] <= kTameResidual;
-            }
-        }
     }
     // every sum of the tile is finite when its three residuals are <= 2^1020
     // (NaN fails the compare): then third_q is RN(s/3) for all of them and the
@@ -509,7 +544,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     auto main_loop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
         for (int ii = 0; ii < ni; ++ii) {
-            const int i = i0 + ii;
+            const int i = ib + i_stride * ii;
             double a13[kColsPerLane];
             {
                 const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
@@ -621,8 +656,8 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     auto full_loop = [&]() {
         constexpr uint64_t kRowBytes = kChunk * sizeof(float);
         uint64_t rp = reinterpret_cast<uint64_t>(args.cube + coff) +
-                      (uint64_t)((int64_t)i0 * M + j0) * kRowBytes;
-        const uint64_t i_step = (uint64_t)M * kRowBytes;
+                      (uint64_t)((int64_t)ib * M + j0) * kRowBytes;
+        const uint64_t i_step = (uint64_t)i_stride * M * kRowBytes;
         for (int ii = 0; ii < ni; ++ii) {
             double a13[kColsPerLane];
             {
@@ -665,7 +700,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
             int32_t mi;
             wave_argmin8_transposed(key, idx, lane, mk, mi);
             if (lane < kCubeRPW) {
-                const int64_t row = roff + (int64_t)(i0 + ii) * M + j0 + lane;
+                const int64_t row = roff + (int64_t)(ib + i_stride * ii) * M + j0 + lane;
                 if (args.argmin) args.argmin[row] = mi;
                 if (args.minval) args.minval[row] = __uint_as_float(mk);
             }
