@@ -63,7 +63,9 @@ def argmin_path(request):
 
 @pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),
                                           (4, 3, 37, True), (2, 2, 1, False), (3, 6, 130, True),
-                                          (1, 3, 2500, False), (3, 2, 1500, True), (1, 8, 300, True)])
+                                          (1, 3, 2500, False), (3, 2, 1500, True), (1, 8, 300, True),
+                                          (3, 4, 1000, True), (2, 3, 800, False), (2, 2, 1021, False),
+                                          (2, 3, 1024, True), (1, 2, 1000, False)])
 def test_pairwise_synthetic_vs_oracle(cuda, S, C, n, ragged, argmin_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, C, n, seed=100 + S * n, ragged=ragged)
@@ -126,6 +128,24 @@ def test_pairwise_edge_cases(cuda, argmin_path):
     F[5] *= 1e-9                # norms near the 1e-8 threshold
     F[7, 2] = 1e70              # huge l2
     assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C, options=argmin_path)
+
+
+def test_pairwise_wide_views_edge_cases(cuda, argmin_path):
+    """Views of 769..1024 columns (C3's shape: several column chunks per
+    wave, the lazy argmin's chunk recovery) with degenerate lines, NaN / inf / huge centroids and a column
+    count that leaves the last wave's lanes partly empty."""
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(3, 3, 900, seed=77)
+    pts = b.pts.copy()
+    o1 = int(b.cam_offs[1])
+    pts[o1 + 5] = [np.nan, 3.0]          # a NaN column (scene 0, camera 1)
+    pts[o1 + 700] = [np.inf, 1.0]
+    pts[7] = [1e300, -1e300]            # a wild row (scene 0, camera 0)
+    pts[int(b.cam_offs[4]) + 3] = [2.0 ** 41, 7.0]
+    F = b.F.copy()
+    F[3, 0:6] = 0.0                     # scene 1, pair (0,1): degenerate row lines
+    F[5, [0, 1, 3, 4, 6, 7]] = 0.0      # scene 1, pair (1,2): degenerate column lines
+    assert_pairwise_equal(cuda, pts, b.cam_offs, F, b.pairs, 3, 3, options=argmin_path)
 
 
 def test_pairwise_ties_and_duplicates(cuda, argmin_path):

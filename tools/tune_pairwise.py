@@ -42,6 +42,7 @@ ap.add_argument("--dets", type=int, default=1024)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--variants", default="default")
 ap.add_argument("--no-dist", action="store_true", help="association only (no matrix output)")
+ap.add_argument("--no-argmin", action="store_true", help="matrices only (no association)")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -51,8 +52,8 @@ pts = torch.from_numpy(b.pts).to(dev)
 co = torch.from_numpy(b.cam_offs).to(dev)
 F = torch.from_numpy(b.F).to(dev)
 dist = torch.empty(0 if args.no_dist else plan.n_dist, dtype=torch.float32, device=dev)
-am = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
-mv = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
+am = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.int32, device=dev)
+mv = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.float32, device=dev)
 nbytes = (16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0] + (0 if args.no_dist else 4.0 * plan.n_dist)
           + 8.0 * plan.n_rows)
 variants = [v.strip() for v in args.variants.split(",")]
