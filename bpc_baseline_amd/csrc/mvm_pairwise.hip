@@ -20,6 +20,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mvmatch.h"
 #include "mvm_device.h"
 #include "mvm_internal.h"
@@ -27,6 +29,8 @@
 #pragma clang fp contract(off)
 
 namespace {
+
+constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 
 // ------------------------------------------------------- pairwise kernel ----
 struct PairArgs {
@@ -150,7 +154,9 @@ __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double 
     }
 }
 
-template <bool STORE, int NT>
+// TRACK: also keep the chunk of the minimum (lazy == 1); lazy == 2 keeps the
+// bits only (two v_min3_u32 per 4 pairs) and recovers the chunk at group end
+template <bool STORE, int NT, bool TRACK>
 __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
                                               double rx, double ry, float *drow, int jbase,
                                               uint32_t &bbits, int32_t &bchunk, int32_t cidx) {
@@ -160,8 +166,18 @@ __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, doub
     const uint32_t m = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]),
                                          __float_as_uint(v[2])),
                                 __float_as_uint(v[3]), bbits);
-    bchunk = (m < bbits) ? cidx : bchunk;
+    if (TRACK) bchunk = (m < bbits) ? cidx : bchunk;
     bbits = m;
+}
+
+// float32 bits of the stored value of column jj (tile-local) against row slot
+// line `rl` = {l0, l1, l2, x, y}: row_fast's arithmetic for one pair
+__device__ __forceinline__ uint32_t pair_bits1(const double *s_l0, const double *s_l1,
+                                               const double *s_l2, const double *s_x,
+                                               const double *s_y, int jj, const double *rl) {
+    const double d1 = __builtin_fma(s_l1[jj], rl[4], s_l0[jj] * rl[3]) + s_l2[jj];
+    const double d2 = __builtin_fma(rl[1], s_y[jj], rl[0] * s_x[jj]) + rl[2];
+    return __float_as_uint((float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2)));
 }
 
 // Column (within the tile) of the first of the 4 values of columns jj0..jj0+3
@@ -262,6 +278,37 @@ __device__ __forceinline__ void lazy_reduce_transposed(uint32_t *red, const uint
     key = group_min_u32<RPW>(key);
     w = (int)(key & 63u);
     c = (int)(key >> 6);
+}
+
+// lazy == 2: the same transpose without chunks.  Returns the row minimum k,
+// the lowest lane w holding it, and whether another lane holds it too (`tie`:
+// with several chunks the lowest lane is then not necessarily the lowest
+// column).  Uniform over the LPR lanes of a row slot.
+template <int RPW>
+__device__ __forceinline__ void lazy_reduce_bits(uint32_t *red, const uint32_t (&bbits)[RPW],
+                                                 int lane, uint32_t &k, int &w, bool &tie) {
+    constexpr int LPR = kWave / RPW;
+    static_assert(RPW <= 32, "lane mask is 32 bits");
+    const int rs = lane / LPR, seg = lane % LPR;
+#pragma unroll
+    for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = bbits[r];
+    uint32_t v[RPW];
+    read_segment<RPW>(red, rs, seg, v);
+    uint32_t m = v[0];
+#pragma unroll
+    for (int i = 1; i < RPW; ++i) m = v[i] < m ? v[i] : m;
+    k = group_min_u32<RPW>(m);
+    uint32_t mask = 0;
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) mask |= (v[i] == k) ? (1u << i) : 0u;
+    const uint32_t base = (uint32_t)(seg * RPW);
+    // first and (complemented) last lane holding k: equal iff exactly one lane
+    const uint32_t lo = mask ? base + (uint32_t)__builtin_ctz(mask) : 0xFFFFFFFFu;
+    const uint32_t hi = mask ? ~(base + 31u - (uint32_t)__builtin_clz(mask)) : 0xFFFFFFFFu;
+    const uint32_t first = group_min_u32<RPW>(lo);
+    const uint32_t last = ~group_min_u32<RPW>(hi);
+    w = (int)first;
+    tie = first != last;
 }
 
 
@@ -418,65 +465,95 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
                 bbits[r] = 0x7F800000u;
                 bchunk[r] = 0;
             }
-            for (int c0 = 0, cidx = 0; c0 < nb; c0 += kChunk, ++cidx) {
-                ColRegs c;
+            auto sweep = [&](auto track) {
+                constexpr bool TRACK = decltype(track)::value;
+                for (int c0 = 0, cidx = 0; c0 < nb; c0 += kChunk, ++cidx) {
+                    ColRegs c;
 #pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
-                    const int jj = c0 + kColsPerLane * lane + q;
-                    c.l0[q] = s_l0[jj];
-                    c.l1[q] = s_l1[jj];
-                    c.l2[q] = s_l2[jj];
-                    c.x[q] = s_x[jj];
-                    c.y[q] = s_y[jj];
-                }
-                const int jbase = c0 + kColsPerLane * lane;
-                if (dbase) {
-                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
-                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) {
-                        row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1],
-                                                rowp[r][2], rowp[r][3],
-                                                rowp[r][4], reinterpret_cast<float *>(rp),
-                                                jbase, bbits[r], bchunk[r], cidx);
-                        rp += rstep;
-                        // keep the row address a running scalar: stops LICM
-                        // hoisting all RPW row bases out of the chunk loop
-                        // (they would be spilled to VGPR lanes)
-                        __asm__ volatile("" : "+s"(rp));
+                    for (int q = 0; q < kColsPerLane; ++q) {
+                        const int jj = c0 + kColsPerLane * lane + q;
+                        c.l0[q] = s_l0[jj];
+                        c.l1[q] = s_l1[jj];
+                        c.l2[q] = s_l2[jj];
+                        c.x[q] = s_x[jj];
+                        c.y[q] = s_y[jj];
                     }
-                } else {
+                    const int jbase = c0 + kColsPerLane * lane;
+                    if (dbase) {
+                        const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                        uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
 #pragma unroll
-                    for (int r = 0; r < RPW; ++r)
-                        row_fast_lazy<false, NT>(c, rowp[r][0], rowp[r][1],
-                                                 rowp[r][2], rowp[r][3],
-                                                 rowp[r][4], nullptr, jbase, bbits[r],
-                                                 bchunk[r], cidx);
+                        for (int r = 0; r < RPW; ++r) {
+                            row_fast_lazy<true, NT, TRACK>(c, rowp[r][0], rowp[r][1],
+                                                           rowp[r][2], rowp[r][3],
+                                                           rowp[r][4], reinterpret_cast<float *>(rp),
+                                                           jbase, bbits[r], bchunk[r], cidx);
+                            rp += rstep;
+                            // keep the row address a running scalar: stops LICM
+                            // hoisting all RPW row bases out of the chunk loop
+                            // (they would be spilled to VGPR lanes)
+                            __asm__ volatile("" : "+s"(rp));
+                        }
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < RPW; ++r)
+                            row_fast_lazy<false, NT, TRACK>(c, rowp[r][0], rowp[r][1],
+                                                            rowp[r][2], rowp[r][3],
+                                                            rowp[r][4], nullptr, jbase, bbits[r],
+                                                            bchunk[r], cidx);
+                    }
                 }
-            }
+            };
             if (args.lazy >= 2) {
+                sweep(std::false_type{});
                 constexpr int LPR = kWave / RPW;
+                constexpr int VPL = kColsPerLane * (kMaxColTile / kChunk) / LPR;
+                static_assert(VPL >= 1 && LPR * VPL == kColsPerLane * (kMaxColTile / kChunk),
+                              "recovery slots");
                 uint32_t k;
-                int w, cw;
-                lazy_reduce_transposed<RPW>(s_red + wave * (RPW * kWave), bbits, bchunk,
-                                            nb > kChunk, lane, k, w, cw);
-                // the LPR lanes of row slot rs recompute the winner's 4 values
-                // (lane seg takes q = seg % 4) and keep the first equal to k
-                const int rs = lane / LPR, q = (lane % LPR) & (kColsPerLane - 1);
-                const int jj = cw * kChunk + kColsPerLane * w + q;
+                int w;
+                bool tie;
+                lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lane, k, w, tie);
+                // the LPR lanes of row slot rs recompute lane w's values in
+                // every chunk (slot idx = chunk * 4 + q; lazy tiles have
+                // nb == T, a multiple of kChunk) and keep the first equal to k
+                const int rs = lane / LPR, seg = lane % LPR;
+                const int n_ch = nb / kChunk;
                 const double *rl = rowp[rs];
-                const double d1 = __builtin_fma(s_l1[jj], rl[4], s_l0[jj] * rl[3]) + s_l2[jj];
-                const double d2 = __builtin_fma(rl[1], s_y[jj], rl[0] * s_x[jj]) + rl[2];
-                const uint32_t b =
-                    __float_as_uint((float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2)));
-                const uint32_t qm = group_min_u32<RPW>((b == k) ? (uint32_t)q : 0xFFFFFFFFu);
-                if (lane % LPR == 0) {
+                uint32_t first = 0xFFFFFFFFu;
+#pragma unroll
+                for (int t = VPL - 1; t >= 0; --t) {
+                    const int idx = seg + LPR * t;
+                    const int c = idx / kColsPerLane, q = idx % kColsPerLane;
+                    if (c < n_ch) {
+                        const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
+                                                      c * kChunk + kColsPerLane * w + q, rl);
+                        first = (b == k) ? (uint32_t)idx : first;
+                    }
+                }
+                first = group_min_u32<RPW>(first);
+                int jwin = (int)(first / kColsPerLane) * kChunk + kColsPerLane * w +
+                           (int)(first % kColsPerLane);
+                // rare: several lanes hold the minimum over several chunks ->
+                // the row slot's lanes scan every column for the first equal to k
+                tie = tie && n_ch > 1;
+                if (__builtin_expect(__any(tie), 0)) {
+                    if (tie) {
+                        uint32_t jt = 0xFFFFFFFFu;
+                        for (int jj = nb - LPR + seg; jj >= 0; jj -= LPR)
+                            jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj, rl) == k)
+                                     ? (uint32_t)jj : jt;
+                        jwin = (int)group_min_u32<RPW>(jt);
+                    }
+                }
+                if (seg == 0) {
                     const int64_t row = row_off0 + grow0 + rs;
-                    if (args.argmin) args.argmin[row] = jj - q + (int)qm;
+                    if (args.argmin) args.argmin[row] = jwin;
                     if (args.minval) args.minval[row] = __uint_as_float(k);
                 }
                 continue;
             }
+            sweep(std::true_type{});
             // per row: wave minimum, its lane and chunk; lane r gathers row r's
             uint32_t my_k = 0;
             int32_t my_l = 0, my_c = 0;
@@ -628,7 +705,6 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
 
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;    // default: 64 rows per row group
-constexpr int kMaxColTile = 1024;   // column lines resident in LDS per workgroup
 constexpr int64_t kMinBlocks = 4096; // ~8 rounds of 2 resident workgroups on 256 CUs
 
 int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
