@@ -302,13 +302,15 @@ def test_launches_capture_into_a_hip_graph(cuda):
                            r.view(torch.int32) if r.dtype == torch.float32 else r)
 
 
-@pytest.mark.parametrize("n", [520, 100, 60])
+@pytest.mark.parametrize("n", [520, 256, 100, 60])
 def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
     """A row's winning k duplicated in its own lane group, in another lane and
     (views of more than 256) in the same lane of the next 256-chunk and in the
     ragged tail chunk; the lowest k must win (the chunked kernel keeps the
     earliest chunk).  n = 100 runs the two-rows-per-wave kernel, with rows in
-    both halves of a wave (wave rows 0..3 and 4..7)."""
+    both halves of a wave (wave rows 0..3 and 4..7); n = 256 runs the fused
+    kernel's full-tile loop, whose in-lane first index comes from lane masks
+    (k0 ^ 1, k0 ^ 2, k0 ^ 3: every q position of the winner's lane)."""
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(1, 3, n, seed=21)
     pts = b.pts.copy()
@@ -316,7 +318,7 @@ def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
     o3 = int(b.cam_offs[2])
     for row in (0, 77, 6 * n + 5):
         k0 = int(ra[row])
-        for k in {k0 ^ 1, (k0 + 256) % n, (k0 + 260) % n, n - 3}:
+        for k in {k0 ^ 1, k0 ^ 2, k0 ^ 3, (k0 + 256) % n, (k0 + 260) % n, n - 3} - {k0}:
             pts[o3 + k] = pts[o3 + k0]
     c, a, m = run_cube(cuda, pts, b.cam_offs, b.F, 1, options=cube_path[1])
     rc, ra, rm, _, _ = O.cube(pts, b.cam_offs, b.F, 1)
