@@ -15,8 +15,12 @@ detections/view x 10,000 scenes, 6 camera pairs -> 6.29e10 detection pairs
 per step.  With N GPUs the 10,000 scenes are split over the ranks (strong
 scaling, the default), so ``--gpus 8`` is configs[3]: 1,250 scenes per GPU;
 ``--scaling weak`` gives every rank its own 10,000.  Scenes are processed in
-equal launches of at most ``--chunk`` scenes; every residual is stored to HBM
-(a launch-sized buffer is reused across launches).
+equal launches of at most ``--chunk`` scenes; every residual is stored to HBM.
+By default every launch of a step writes its own output allocation (C3: ten
+25 GB matrices buffers, 253 GB), so a step's outputs all stay resident and
+the measurement covers most of the HBM rather than wherever one launch-sized
+buffer happened to land (the same launch runs up to ~20% apart on different
+allocations: DESIGN.md §5); ``--output ring`` reuses as few buffers as fit.
 
 Printed by rank 0: ONE JSON line with value = total pairs/s over all ranks,
 the dominant kernel's roofline (achieved algorithmic GB/s from HIP events on
@@ -198,22 +202,37 @@ def cpu_baseline(batch, mode: str, target_s: float):
 
 
 class ClockSampler:
-    """Samples the GPU's current shader clock (the starred level of
-    /sys/class/drm/card*/device/pp_dpm_sclk) on a host thread while the timed
-    region runs, so box-to-box spread can be attributed to clocks or not."""
+    """Samples the GPU's current clock levels (the starred line of
+    /sys/class/drm/card*/device/pp_dpm_{sclk,mclk,fclk}) on a host thread while
+    the timed region runs, so run-to-run and box-to-box spread can be
+    attributed to clocks or not."""
+
+    KINDS = ("sclk", "mclk", "fclk")
 
     def __init__(self, period_s: float = 0.01):
         import glob
         import threading
-        self.paths = sorted(glob.glob("/sys/class/drm/card*/device/pp_dpm_sclk"))
+        self.paths = {k: sorted(glob.glob(f"/sys/class/drm/card*/device/pp_dpm_{k}"))
+                      for k in self.KINDS}
         self.period = period_s
-        self.samples = []
+        self.samples = {k: [] for k in self.KINDS}
+        # hwmon temperatures by label (edge / junction / mem), degrees C
+        self.temp_paths = {}
+        for lab in sorted(glob.glob("/sys/class/drm/card*/device/hwmon/hwmon*/temp*_label")):
+            try:
+                with open(lab) as fh:
+                    name = fh.read().strip()
+            except OSError:
+                continue
+            self.temp_paths.setdefault(name, []).append(lab[:-len("label")] + "input")
+        self.temps = {k: [] for k in self.temp_paths}
         self.stop_ev = threading.Event()
         self.thread = threading.Thread(target=self._run, daemon=True)
 
-    def _read(self):
+    @staticmethod
+    def _read(paths):
         vals = []
-        for p in self.paths:
+        for p in paths:
             try:
                 with open(p) as fh:
                     for line in fh:
@@ -225,13 +244,24 @@ class ClockSampler:
 
     def _run(self):
         while not self.stop_ev.is_set():
-            v = self._read()
-            if v is not None:
-                self.samples.append(v)
+            for k in self.KINDS:
+                v = self._read(self.paths[k])
+                if v is not None:
+                    self.samples[k].append(v)
+            for name, paths in self.temp_paths.items():
+                vals = []
+                for p in paths:
+                    try:
+                        with open(p) as fh:
+                            vals.append(int(fh.read().strip()) / 1000.0)
+                    except (OSError, ValueError):
+                        pass
+                if vals:
+                    self.temps[name].append(max(vals))
             self.stop_ev.wait(self.period)
 
     def __enter__(self):
-        if self.paths:
+        if any(self.paths.values()):
             self.thread.start()
         return self
 
@@ -240,11 +270,20 @@ class ClockSampler:
         if self.thread.is_alive():
             self.thread.join()
 
-    def summary(self):
-        if not self.samples:
-            return {"source": "pp_dpm_sclk unreadable", "samples": 0}
-        s = np.asarray(self.samples, dtype=np.float64)
-        return {"source": "pp_dpm_sclk (starred level, max over visible cards)",
+    def temperatures(self):
+        """Max over visible cards per hwmon label, first and last sample of the
+        timed region (degrees C): HBM above ~85 C refreshes twice as often."""
+        out = {}
+        for name, v in self.temps.items():
+            if v:
+                out[name] = {"first_c": v[0], "last_c": v[-1], "max_c": max(v)}
+        return out or None
+
+    def summary(self, kind: str = "sclk"):
+        if not self.samples[kind]:
+            return {"source": f"pp_dpm_{kind} unreadable", "samples": 0}
+        s = np.asarray(self.samples[kind], dtype=np.float64)
+        return {"source": f"pp_dpm_{kind} (starred level, max over visible cards)",
                 "samples": int(s.size), "mean_mhz": float(s.mean()), "min_mhz": float(s.min()),
                 "max_mhz": float(s.max())}
 
@@ -281,6 +320,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target length of the CPU-baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--output", choices=["resident", "ring"], default="resident",
+                    help="resident (default): one output allocation per launch of a step, when "
+                         "HBM holds them (else as many as fit, reused round robin); ring: one")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay each step's launches as one hipGraph (auto: on for a single GPU, "
                          "where the step has no collective)")
@@ -315,19 +357,29 @@ def main():
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
     max_units = max(c.units for c in chunks)
-    dist_buf = torch.empty(max_units, dtype=torch.float32, device=dev)
+    # output slots: one allocation per launch of the step when they fit (all
+    # of a step's residuals stay resident), keeping >= 4 GB of HBM free
+    n_slots = 1
+    if args.output == "resident":
+        free, _ = torch.cuda.mem_get_info(dev)
+        n_slots = int(max(1, min(len(chunks), (free - (4 << 30)) // (4 * max_units))))
+    out_slots = [torch.empty(max_units, dtype=torch.float32, device=dev) for _ in range(n_slots)]
+    slot_of = {id(c): k % n_slots for k, c in enumerate(chunks)}
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
+
+    def out_of(c: Chunk):
+        return out_slots[slot_of[id(c)]][:c.units]
 
     def launch(c: Chunk):
         am = argmin[c.row_base:c.row_base + c.plan.n_rows]
         mv = minval[c.row_base:c.row_base + c.plan.n_rows]
         if wl["mode"] == "pairwise":
             ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan,
-                                         out=(dist_buf[:c.units], am, mv))
+                                         out=(out_of(c), am, mv))
         else:
             ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan,
-                                    out=(dist_buf[:c.units], am, mv))
+                                    out=(out_of(c), am, mv))
 
     # the single association gather (N > 1), in per-launch pieces that overlap
     # the next launch's compute; ragged shards fall back to one gather at the end
@@ -457,7 +509,7 @@ def main():
     parity = "skipped"
     if env.is_root and wl["mode"] == "pairwise":
         from oracle import oracle as O
-        c = chunks[-1]          # its residuals are still in dist_buf
+        c = chunks[-1]          # its residuals are still in its output slot
         s_first = c.s0
         C = batch.n_cams
         co = batch.cam_offs[s_first * C:(s_first + 1) * C + 1]
@@ -465,18 +517,18 @@ def main():
         rd, ra, _, _, _ = O.pairwise(batch.pts[int(co[0]):int(co[-1])], co_rel,
                                      batch.F[s_first * batch.n_pairs:(s_first + 1) * batch.n_pairs],
                                      batch.pairs, 1, C)
-        gd = dist_buf[:rd.size].cpu().numpy()
+        gd = out_of(c)[:rd.size].cpu().numpy()
         ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
         ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
         parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rd.size} pairs)"
     elif env.is_root:
         from oracle import oracle as O
-        c = chunks[-1]          # its cube is still in dist_buf
+        c = chunks[-1]          # its cube is still in its output slot
         s_first = c.s0
         co = batch.cam_offs[s_first * 3:(s_first + 1) * 3 + 1]
         rc, ra, _, _, _ = O.cube(batch.pts[int(co[0]):int(co[-1])], co - co[0],
                                  batch.F[s_first * 3:(s_first + 1) * 3], 1)
-        gc = dist_buf[:rc.size].cpu().numpy()
+        gc = out_of(c)[:rc.size].cpu().numpy()
         ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
         ok = np.array_equal(gc.view(np.int32), rc.view(np.int32)) and np.array_equal(ga, ra)
         parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rc.size} triples)"
@@ -512,17 +564,20 @@ def main():
                          "+ offsets + F, kernel, D2H argmin/min (best of 3); the distance matrices "
                          "stay in HBM")}
 
-    # ---- achievable HBM write bandwidth on this box (same store form) -------
+    # ---- achievable HBM write bandwidth on this box (same store form), over
+    # the same output allocations the launches wrote ----------------------------
     probe_gbs = None
     if env.is_root:
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ops.hbm_write_probe(dist_buf)
+        for buf in out_slots:
+            ops.hbm_write_probe(buf)
         pe0.record(stream)
         for _ in range(5):
-            ops.hbm_write_probe(dist_buf)
+            for buf in out_slots:
+                ops.hbm_write_probe(buf)
         pe1.record(stream)
         torch.cuda.synchronize(dev)
-        probe_gbs = 5 * dist_buf.numel() * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
+        probe_gbs = 5 * n_slots * max_units * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
 
 
     units_all = sum_over_ranks(env, units_local)   # ragged shards differ by one scene
@@ -554,6 +609,8 @@ def main():
             "n_scenes_per_gpu": n_local,
             "n_scenes_total": n_local * world if args.scaling == "weak" else wl["n_scenes"],
             "scenes_per_launch": chunk, "launches_per_step": len(chunks),
+            "output_allocations": n_slots,
+            "output_gb": n_slots * max_units * 4 / 1e9,
             "units_per_gpu_step": units_local,
             "launch": ("one hipGraph holding the K steps' launches, captured once outside the "
                        "timed region, replayed once" if graph is not None else "eager op calls"),
@@ -568,7 +625,10 @@ def main():
                            "source": "torch.distributed.get_world_size()/get_backend() after init"}
                           if env.initialised else None),
         "step_split": split,
-        "sclk": clocks.summary(),
+        "sclk": clocks.summary("sclk"),
+        "mclk": clocks.summary("mclk"),
+        "fclk": clocks.summary("fclk"),
+        "temperature": clocks.temperatures(),
         "roofline": {
             "bound": "hbm",
             "kernel": ("pairwise_kernel" if wl["mode"] == "pairwise"
