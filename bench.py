@@ -363,7 +363,15 @@ def main():
     if args.output == "resident":
         free, _ = torch.cuda.mem_get_info(dev)
         n_slots = int(max(1, min(len(chunks), (free - (4 << 30)) // (4 * max_units))))
-    out_slots = [torch.empty(max_units, dtype=torch.float32, device=dev) for _ in range(n_slots)]
+    out_slots = []
+    for _ in range(n_slots):   # fewer if the allocator refuses one (fragmented HBM)
+        try:
+            out_slots.append(torch.empty(max_units, dtype=torch.float32, device=dev))
+        except torch.cuda.OutOfMemoryError:
+            if not out_slots:
+                raise
+            break
+    n_slots = len(out_slots)
     slot_of = {id(c): k % n_slots for k, c in enumerate(chunks)}
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
