@@ -288,6 +288,15 @@ class ClockSampler:
                 "max_mhz": float(s.max())}
 
 
+def output_slots(n_launch: int, slot_bytes: int, free_bytes: int,
+                 reserve_bytes: int = 4 << 30) -> int:
+    """Output allocations for a step: one per launch when HBM holds them with
+    ``reserve_bytes`` to spare, else as many as fit (launches reuse them round
+    robin), never fewer than one."""
+    fit = (free_bytes - reserve_bytes) // slot_bytes if slot_bytes > 0 else n_launch
+    return int(max(1, min(n_launch, fit)))
+
+
 def load_traffic(workload: str, scenes_per_launch: int):
     """PMC-measured HBM bytes per launch (profiles/pmc_traffic.json), only if it
     was collected on this workload at this launch size."""
@@ -361,8 +370,7 @@ def main():
     # of a step's residuals stay resident), keeping >= 4 GB of HBM free
     n_slots = 1
     if args.output == "resident":
-        free, _ = torch.cuda.mem_get_info(dev)
-        n_slots = int(max(1, min(len(chunks), (free - (4 << 30)) // (4 * max_units))))
+        n_slots = output_slots(len(chunks), 4 * max_units, torch.cuda.mem_get_info(dev)[0])
     out_slots = []
     for _ in range(n_slots):   # fewer if the allocator refuses one (fragmented HBM)
         try:

@@ -352,3 +352,15 @@ def test_rig_matrices_dedupe_bit_equal(mode):
     F, P = rig_matrices(Ks, RTs)
     assert np.array_equal(F.view(np.int64), fundamental_matrices_batched(Ks, RTs, camera_pairs(3)).view(np.int64))
     assert np.array_equal(P.view(np.int64), projection_matrices(Ks, RTs).view(np.int64))
+
+
+def test_bench_output_slots():
+    """bench.py gives each launch of a step its own output allocation when HBM
+    holds them with 4 GiB to spare, else as many as fit, never fewer than one."""
+    import bench
+    gib = 1 << 30
+    assert bench.output_slots(10, 25 * gib, 287 * gib) == 10      # C3 on one MI355X
+    assert bench.output_slots(10, 25 * gib, 150 * gib) == 5
+    assert bench.output_slots(10, 25 * gib, 20 * gib) == 1
+    assert bench.output_slots(4, 17 * gib, 287 * gib) == 4        # the C2 cube
+    assert bench.output_slots(1, gib, 287 * gib) == 1
