@@ -317,10 +317,11 @@ __device__ __forceinline__ void lazy_reduce_bits(uint32_t *red, const uint32_t (
 // workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
 // chunk every lane holds 4 consecutive columns in registers and walks the
 // RPW rows, one coalesced 16-byte store per lane per row.
-// occupancy: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
-// (RPW 16 at 4 waves/SIMD spills and measured slower: DESIGN.md §3.1)
-template <int RPW, bool ARGMIN, typename OutT, int NT = 1>
-__global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(PairArgs args) {
+// occupancy OCC: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
+// (RPW 16 at 4 waves/SIMD spills and measured slower: DESIGN.md §3.1); 2 when
+// the workgroup's LDS allows no more anyway (the host picks it)
+template <int RPW, bool ARGMIN, typename OutT, int NT = 1, int OCC = (RPW >= 16 ? 3 : 4)>
+__global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int T = args.col_tile;
     double *s_l0 = reinterpret_cast<double *>(s_dyn);
@@ -706,6 +707,7 @@ __global__ __launch_bounds__(kThreads, RPW >= 16 ? 3 : 4) void pairwise_kernel(P
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;       // default: 64 rows per row group
 constexpr int kDefaultBlockRows = 128; // default rows per workgroup
+constexpr size_t kLds3PerCU = (160u << 10) / 3;   // most LDS a workgroup may take for 3 per CU
 
 int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
                int n_cams) {
@@ -758,6 +760,16 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     // nontemporal stores for whole-line rows; rows that end mid-line share
     // that line with the next row, and L2 must merge it (default policy)
     if (max_cols % 32 == 0) {
+        // LDS allows at most two workgroups per CU (> 160 KiB / 3; C3's 1,024
+        // column lines): the register cap of three waves per SIMD buys nothing
+        // there, and at 168 VGPRs the kernel spills -- a scratch reload ahead
+        // of the lazy chunk loop makes the compiler drain every outstanding
+        // store (s_waitcnt vmcnt(0)) at each chunk.  At two waves per SIMD it
+        // has 200 VGPRs, no spills and no drain: C3 4.21 -> 4.14 ms per launch
+        // on the same four output buffers, build order rotated
+        // (tools/ab_same_buffers.py, profiles/r02/alloc/c3_occ2_same_buffers.log)
+        if (argmin && lds > kLds3PerCU)
+            return launch_lds(pairwise_kernel<RPW, true, float, 1, 2>, grid, block, lds, stream, a);
         if (argmin) return launch_lds(pairwise_kernel<RPW, true, float, 1>, grid, block, lds, stream, a);
         return launch_lds(pairwise_kernel<RPW, false, float, 1>, grid, block, lds, stream, a);
     }

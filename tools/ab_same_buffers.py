@@ -3,7 +3,9 @@ the SAME output buffers.  The launch time depends on where in HBM the output
 lands (tools/probe_alloc.py: the same cube launch runs 2.38-2.45 ms on some
 16.9 GB allocations and 2.95-2.99 ms on others), so builds compared in
 separate processes are confounded by placement; here every build writes
-every buffer, interleaved, and the table is per buffer.
+every buffer, interleaved, and the table is per buffer.  The order of the
+builds rotates every round: the build timed first on a buffer can differ from
+the others by a few % for reasons of position alone.
 
 python tools/ab_same_buffers.py --libs lib/a.so,lib/b.so [--workload cube|c3]
                                 [--buffers 6] [--rounds 3]
@@ -23,7 +25,7 @@ from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--libs", required=True)
-ap.add_argument("--workload", choices=["cube", "c3"], default="cube")
+ap.add_argument("--workload", choices=["cube", "c3", "c2"], default="cube")
 ap.add_argument("--buffers", type=int, default=6)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--scenes", type=int, default=None, help="scenes per launch (cube 250, c3 1000)")
@@ -101,7 +103,8 @@ if args.workload == "cube":
     plan = ops.TripletPlan(b.cam_offs, b.n_scenes, device=dev)
     n_out = plan.n_cube
 else:
-    b = make_scenes(args.scenes or 1000, 4, 1024, seed=0)
+    b = (make_scenes(args.scenes or 1000, 3, 256, seed=0) if args.workload == "c2"
+         else make_scenes(args.scenes or 1000, 4, 1024, seed=0))
     plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
     n_out = plan.n_dist
     pa = (ctypes.c_int32 * len(plan.pair_a))(*plan.pair_a)
@@ -127,24 +130,29 @@ def launch(lib, out):
 
 
 kinds = args.alloc.split(",") if args.alloc else ["torch"] * args.buffers
+reps = 20 if args.workload == "c2" else 3
 bufs = [torch.empty(n_out, dtype=torch.float32, device=dev) if k == "torch"
         else vmm_buffer(n_out, int(k.split(":")[1])) for k in kinds]
 times = {(n, i): [] for n in libs for i in range(len(bufs))}
 ptimes = {i: [] for i in range(len(bufs))}
 ev = lambda: torch.cuda.Event(enable_timing=True)   # noqa: E731
 for rnd in range(args.rounds + 1):
+    names = list(libs)
+    k = rnd % len(names)
+    order = names[k:] + names[:k]   # rotate: every build takes every position (order bias)
     for i, out in enumerate(bufs):
         ref = None
-        for name, lib in libs.items():
+        for name in order:
+            lib = libs[name]
             launch(lib, out)
             e0, e1 = ev(), ev()
             e0.record()
-            for _ in range(3):
+            for _ in range(reps):
                 launch(lib, out)
             e1.record()
             torch.cuda.synchronize()
             if rnd:
-                times[(name, i)].append(e0.elapsed_time(e1) / 3)
+                times[(name, i)].append(e0.elapsed_time(e1) / reps)
             if rnd == 0:   # every build's results equal the first's on this buffer
                 chk = (am.cpu().numpy().tobytes(), out[:1 << 22].cpu().numpy().tobytes(),
                        out[-(1 << 22):].cpu().numpy().tobytes())
