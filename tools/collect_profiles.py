@@ -13,8 +13,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(REPO, "gpurun_out")
 DST = os.path.join(REPO, "profiles", ROUND)
 # kernels that together form one bench launch (the op), per workload
-OP_KERNELS = {"c3": ["pairwise_kernel<16, true, float, 1>"],
-              "c2": ["pairwise_kernel<16, true, float, 1>"],
+OP_KERNELS = {"c3": ["pairwise_kernel<16, true, float, 1"],
+              "c2": ["pairwise_kernel<16, true, float, 1"],
               "c2cube": ["triplet_fused_kernel"]}
 
 
