@@ -957,10 +957,24 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
             lsap_wave_kernel<CT, 1><<<wgrid, wblock, 0, s>>>(a, n_problems);
             empty_done = true;
         }
-        if (wave_max > 64 && overlaps(65, 128)) lsap_wave_kernel<CT, 2><<<wgrid, wblock, 0, s>>>(a, n_problems);
-        if (wave_max > 128 && overlaps(129, 256)) lsap_wave_kernel<CT, 4><<<wgrid, wblock, 0, s>>>(a, n_problems);
-        if (wave_max > 256 && overlaps(257, 512)) lsap_wave_kernel<CT, 8><<<wgrid, wblock, 0, s>>>(a, n_problems);
-        if (wave_max > 512 && overlaps(513, 1024)) lsap_wave_kernel<CT, 16><<<wgrid, wblock, 0, s>>>(a, n_problems);
+        // every instantiation also writes status 0 for the empty problems, so
+        // any one launched spares the workgroup kernel's launch for them
+        if (wave_max > 64 && overlaps(65, 128)) {
+            lsap_wave_kernel<CT, 2><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
+        if (wave_max > 128 && overlaps(129, 256)) {
+            lsap_wave_kernel<CT, 4><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
+        if (wave_max > 256 && overlaps(257, 512)) {
+            lsap_wave_kernel<CT, 8><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
+        if (wave_max > 512 && overlaps(513, 1024)) {
+            lsap_wave_kernel<CT, 16><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
     }
     const bool big = long_max > wave_max;   // anything left for the workgroup kernels
     // Few large problems: G co-resident workgroups per problem (cooperative

@@ -53,25 +53,34 @@ __global__ __launch_bounds__(kPackThreads) void pack_count_kernel(
 // exclusive prefix of the counts -> CSR offsets (one workgroup; chunked scan)
 __global__ __launch_bounds__(1024) void pack_scan_kernel(const int32_t *counts, int32_t n,
                                                          int64_t *offs) {
-    __shared__ int64_t s_part[1024];
-    const int t = threadIdx.x;
+    // each thread sums a contiguous range; the 1024 partial sums are scanned
+    // with wave shuffles (64 lanes) and once more over the 16 wave totals
+    __shared__ int64_t s_wave[16];
+    const int t = threadIdx.x, lane = t % 64, wave = t / 64;
     const int64_t per = (n + 1023) / 1024;
     const int64_t b = (int64_t)t * per, e = min<int64_t>(n, b + per);
     int64_t sum = 0;
     for (int64_t k = b; k < e; ++k) sum += counts[k];
-    s_part[t] = sum;
+    int64_t x = sum;                                  // inclusive scan in the wave
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) s_wave[wave] = x;
     __syncthreads();
-    if (t == 0) {
-        int64_t run = 0;
-        for (int k = 0; k < 1024; ++k) {
-            const int64_t v = s_part[k];
-            s_part[k] = run;
-            run += v;
+    if (wave == 0) {                                  // inclusive scan of the wave totals
+        int64_t w = lane < 16 ? s_wave[lane] : 0;
+#pragma unroll
+        for (int d = 1; d < 16; d <<= 1) {
+            const int64_t y = __shfl_up(w, d, 64);
+            if (lane >= d) w += y;
         }
-        offs[n] = run;
+        if (lane < 16) s_wave[lane] = w;
     }
     __syncthreads();
-    int64_t run = s_part[t];
+    int64_t run = x - sum + (wave > 0 ? s_wave[wave - 1] : 0);   // exclusive prefix
+    if (t == 1023) offs[n] = run + sum;
     for (int64_t k = b; k < e; ++k) {
         offs[k] = run;
         run += counts[k];
