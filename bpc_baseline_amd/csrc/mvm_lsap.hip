@@ -573,7 +573,7 @@ __device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_
     if (lane == 0) a.status[p] = 0;
 }
 
-template <typename CT, int K>
+template <typename CT, int K, int LO = (K > 1 ? 32 * K : 0)>
 __global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs a, int32_t n) {
     __shared__ double s_u[kWaveProblems][64 * K];      // rows <= long side <= 64 K
     __shared__ int32_t s_c4r[kWaveProblems][64 * K];
@@ -588,8 +588,8 @@ __global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs 
         return;
     }
     if (nc > a.wave_max_cols) return;
-    // each instantiation owns the long sides (32K, 64K]: its own register budget
-    if (nc > 64 * K || (K > 1 && nc <= 32 * K)) return;
+    // each instantiation owns the long sides (LO, 64K]: its own register budget
+    if (nc > 64 * K || nc <= LO) return;
     lsap_wave_solve<CT, K>(a, p, R, Kc, s_u[wave], s_c4r[wave], lane);
 }
 
@@ -971,8 +971,14 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
             lsap_wave_kernel<CT, 8><<<wgrid, wblock, 0, s>>>(a, n_problems);
             empty_done = true;
         }
-        if (wave_max > 512 && overlaps(513, 1024)) {
-            lsap_wave_kernel<CT, 16><<<wgrid, wblock, 0, s>>>(a, n_problems);
+        // 12 columns per lane for long sides of 513-768 (576 x 24 at 24
+        // detections per view): a quarter fewer slots per Dijkstra step than 16
+        if (wave_max > 512 && overlaps(513, 768)) {
+            lsap_wave_kernel<CT, 12, 512><<<wgrid, wblock, 0, s>>>(a, n_problems);
+            empty_done = true;
+        }
+        if (wave_max > 768 && overlaps(769, 1024)) {
+            lsap_wave_kernel<CT, 16, 768><<<wgrid, wblock, 0, s>>>(a, n_problems);
             empty_done = true;
         }
     }

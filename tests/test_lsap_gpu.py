@@ -45,7 +45,7 @@ def test_random_shapes_and_ties_batched(cuda, lsap_path):
     mats = []
     for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0),
                   (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70),
-                  (4096, 6), (6, 4096), (2500, 11), (4097, 3)]:
+                  (4096, 6), (6, 4096), (2500, 11), (4097, 3), (513, 7), (768, 5), (5, 768), (769, 4)]:
         for trial in range(4):
             c = rng.normal(size=shape).astype(np.float32)
             if trial == 1:
