@@ -16,11 +16,12 @@ per step.  With N GPUs the 10,000 scenes are split over the ranks (strong
 scaling, the default), so ``--gpus 8`` is configs[3]: 1,250 scenes per GPU;
 ``--scaling weak`` gives every rank its own 10,000.  Scenes are processed in
 equal launches of at most ``--chunk`` scenes; every residual is stored to HBM.
-By default every launch of a step writes its own output allocation (C3: ten
-25 GB matrices buffers, 253 GB), so a step's outputs all stay resident and
-the measurement covers most of the HBM rather than wherever one launch-sized
-buffer happened to land (the same launch runs up to ~20% apart on different
-allocations: DESIGN.md §5); ``--output ring`` reuses as few buffers as fit.
+By default every launch of the timed steps writes its own output allocation
+as far as HBM holds them (C3: ten 25 GB buffers, 252 GB, one per launch of a
+step; C2: one per step), taken round robin, so a step's outputs all stay
+resident and the measurement covers much of the HBM rather than wherever one
+launch-sized buffer happened to land (the same launch runs up to ~20% apart
+on different allocations: DESIGN.md §5); ``--output ring`` reuses one buffer.
 
 Printed by rank 0: ONE JSON line with value = total pairs/s over all ranks,
 the dominant kernel's roofline (achieved algorithmic GB/s from HIP events on
@@ -289,7 +290,7 @@ class ClockSampler:
 
 
 def output_slots(n_launch: int, slot_bytes: int, free_bytes: int,
-                 reserve_bytes: int = 4 << 30) -> int:
+                 reserve_bytes: int = 8 << 30) -> int:
     """Output allocations for a step: one per launch when HBM holds them with
     ``reserve_bytes`` to spare, else as many as fit (launches reuse them round
     robin), never fewer than one."""
@@ -330,8 +331,8 @@ def main():
                     help="target length of the CPU-baseline sample (0 disables)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--output", choices=["resident", "ring"], default="resident",
-                    help="resident (default): one output allocation per launch of a step, when "
-                         "HBM holds them (else as many as fit, reused round robin); ring: one")
+                    help="resident (default): one output allocation per launch of the timed "
+                         "steps as far as HBM holds them (reused round robin); ring: one")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                     help="replay each step's launches as one hipGraph (auto: on for a single GPU, "
                          "where the step has no collective)")
@@ -366,11 +367,14 @@ def main():
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
     max_units = max(c.units for c in chunks)
-    # output slots: one allocation per launch of the step when they fit (all
-    # of a step's residuals stay resident), keeping >= 4 GB of HBM free
+    # output slots: one allocation per launch of the timed steps when they fit
+    # (a step's residuals all stay resident, and consecutive steps write other
+    # allocations, as a service that double-buffers its outputs would),
+    # keeping >= 8 GiB of HBM free (RCCL, the gather); launches take the slots round robin
     n_slots = 1
     if args.output == "resident":
-        n_slots = output_slots(len(chunks), 4 * max_units, torch.cuda.mem_get_info(dev)[0])
+        n_slots = output_slots(len(chunks) * max(1, args.steps), 4 * max_units,
+                               torch.cuda.mem_get_info(dev)[0])
     out_slots = []
     for _ in range(n_slots):   # fewer if the allocator refuses one (fragmented HBM)
         try:
@@ -380,22 +384,24 @@ def main():
                 raise
             break
     n_slots = len(out_slots)
-    slot_of = {id(c): k % n_slots for k, c in enumerate(chunks)}
+    seq = [0]             # launches issued (or captured) so far: the next slot
+    last_slot = {}        # chunk -> the slot its latest launch wrote
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
 
     def out_of(c: Chunk):
-        return out_slots[slot_of[id(c)]][:c.units]
+        return out_slots[last_slot[id(c)]][:c.units]
 
     def launch(c: Chunk):
         am = argmin[c.row_base:c.row_base + c.plan.n_rows]
         mv = minval[c.row_base:c.row_base + c.plan.n_rows]
+        last_slot[id(c)] = seq[0] % n_slots
+        seq[0] += 1
+        out = out_slots[last_slot[id(c)]][:c.units]
         if wl["mode"] == "pairwise":
-            ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan,
-                                         out=(out_of(c), am, mv))
+            ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
         else:
-            ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan,
-                                    out=(out_of(c), am, mv))
+            ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
 
     # the single association gather (N > 1), in per-launch pieces that overlap
     # the next launch's compute; ragged shards fall back to one gather at the end
@@ -426,6 +432,7 @@ def main():
         step()
     torch.cuda.synchronize(dev)
     env.barrier()
+    seq[0] = 0            # the timed steps start at slot 0
 
     # ---- single GPU: the K timed steps as ONE hipGraph (captured once,
     # outside the timed region), so the launches of consecutive steps run back
@@ -445,6 +452,7 @@ def main():
         graph.replay()
         torch.cuda.synchronize(dev)
         step_bytes = sum(c.nbytes for c in chunks)
+        seq[0] = 0
 
     events = []
     gathered = None

@@ -706,7 +706,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
 
 // ------------------------------------------------------------ host side ----
 constexpr int kRowsPerWave = 16;       // default: 64 rows per row group
-constexpr int kDefaultBlockRows = 128; // default rows per workgroup
+constexpr int64_t kMinBlocks = 4096;   // ~8 rounds of two resident workgroups on 256 CUs
 constexpr size_t kLds3PerCU = (160u << 10) / 3;   // most LDS a workgroup may take for 3 per CU
 
 int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_pairs,
@@ -795,18 +795,23 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
                         (int)o.pairwise_row_groups);
-    // default: row blocks of ~128 rows (never more than the view has).  The
-    // column lines are amortised over fewer rows than with 256-row blocks,
-    // but the XCD's concurrently written region halves, and that is what
-    // decides the speed on HBM regions that stream slowly: over ten 25 GB
-    // output allocations of one process, C3 took 4.10-4.32 ms per launch with
-    // 256-row blocks and 4.13-4.18 ms with 128 (means 4.18 / 4.15;
-    // tools/probe_alloc.py).  C2 (3,000 matrices of 256 rows)
-    // also needs the 6,000 blocks to fill the last round of workgroups.
+    // default: enough row groups to amortise the column lines over ~256 rows,
+    // never more than the rows a view has -- halved to ~128 rows while the
+    // grid has fewer than kMinBlocks workgroups: the last round of long-lived
+    // workgroups is a tail with idle CUs (C2, 3,000 matrices of 256 rows:
+    // 0.156 -> 0.143 ms per launch).  C3 keeps 256: at two waves per SIMD
+    // (no spills, no store drain) its 256-row blocks measured 4.08 vs 4.20 ms
+    // per launch over eight output buffers.
     const int groups_needed = (max_rows + kWaves * rpw - 1) / (kWaves * rpw);
     const int64_t sp_count = (int64_t)n_scenes * a.n_pairs;
     int rg = o.pairwise_row_groups;
-    if (!rg) rg = max(1, min(groups_needed, kDefaultBlockRows / (kWaves * rpw)));
+    if (!rg) {
+        rg = max(1, min(groups_needed, 256 / (kWaves * rpw)));
+        const int rg_floor = min(rg, max(1, 128 / (kWaves * rpw)));
+        while (rg > rg_floor &&
+               sp_count * ((max_rows + kWaves * rpw * rg - 1) / (kWaves * rpw * rg)) < kMinBlocks)
+            rg /= 2;
+    }
     const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
     const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
     if (blocks > 0x7FFFFFFFLL)

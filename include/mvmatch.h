@@ -92,7 +92,7 @@ typedef struct mvm_options {
     int32_t size;                   /* sizeof(mvm_options) */
     int32_t pairwise_argmin;        /* MVM_PAIRWISE_ARGMIN_* */
     int32_t pairwise_rows_per_wave; /* 0 default (16); 4, 8 or 16 */
-    int32_t pairwise_row_groups;    /* 0 default (~128 rows per workgroup); 1..16 */
+    int32_t pairwise_row_groups;    /* 0 default (~256 rows per workgroup, ~128 for small grids); 1..16 */
     int32_t cube_kernel;            /* MVM_CUBE_* */
     int32_t cube_rows_per_instr;    /* FUSED: 0 default (by view size); 1, 2 or 4
                                        (i, j) rows per wave instruction, capped by

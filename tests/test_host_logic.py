@@ -355,12 +355,13 @@ def test_rig_matrices_dedupe_bit_equal(mode):
 
 
 def test_bench_output_slots():
-    """bench.py gives each launch of a step its own output allocation when HBM
-    holds them with 4 GiB to spare, else as many as fit, never fewer than one."""
+    """bench.py gives each launch of the timed steps its own output allocation
+    as far as HBM holds them with 8 GiB to spare, never fewer than one."""
     import bench
     gib = 1 << 30
-    assert bench.output_slots(10, 25 * gib, 287 * gib) == 10      # C3 on one MI355X
+    assert bench.output_slots(10 * 20, 25 * gib, 287 * gib) == 11   # C3 on one MI355X
     assert bench.output_slots(10, 25 * gib, 150 * gib) == 5
     assert bench.output_slots(10, 25 * gib, 20 * gib) == 1
-    assert bench.output_slots(4, 17 * gib, 287 * gib) == 4        # the C2 cube
+    assert bench.output_slots(4 * 20, 17 * gib, 287 * gib) == 16    # the C2 cube
+    assert bench.output_slots(20, gib, 287 * gib) == 20             # C2: one per step
     assert bench.output_slots(1, gib, 287 * gib) == 1
