@@ -511,14 +511,22 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                 constexpr int VPL = kColsPerLane * (kMaxColTile / kChunk) / LPR;
                 static_assert(VPL >= 1 && LPR * VPL == kColsPerLane * (kMaxColTile / kChunk),
                               "recovery slots");
+                // the lane id as a fresh value per group: everything derived
+                // from it here (row slot, LDS and output addresses) is then
+                // recomputed per group instead of hoisted out of the group loop
+                // and spilled -- at 3 waves/SIMD (C2) those spills were reloaded
+                // after the group's stores, and the in-order vmcnt wait for the
+                // reload drained all of them
+                int lz = lane;
+                __asm__ volatile("" : "+v"(lz));
                 uint32_t k;
                 int w;
                 bool tie;
-                lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lane, k, w, tie);
+                lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lz, k, w, tie);
                 // the LPR lanes of row slot rs recompute lane w's values in
                 // every chunk (slot idx = chunk * 4 + q; lazy tiles have
                 // nb == T, a multiple of kChunk) and keep the first equal to k
-                const int rs = lane / LPR, seg = lane % LPR;
+                const int rs = lz / LPR, seg = lz % LPR;
                 const int n_ch = nb / kChunk;
                 const double *rl = rowp[rs];
                 uint32_t first = 0xFFFFFFFFu;
@@ -698,7 +706,9 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                 imin[r] = 0;
                 if (r < nrows) wave_argmin(best_key(best[r]), best[r].j, kmin[r], imin[r]);
             }
-            store_row_results<RPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+            int lz = lane;   // fresh per group: no hoisted, spilled row addresses
+            __asm__ volatile("" : "+v"(lz));
+            store_row_results<RPW>(kmin, imin, nrows, lz, args.argmin, args.minval,
                                    row_off0 + grow0);
         }
     }
