@@ -130,6 +130,27 @@ def test_pairwise_edge_cases(cuda, argmin_path):
     assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C, options=argmin_path)
 
 
+@pytest.mark.parametrize("counts", [(1000, 996, 1016, 1012), (72, 100, 132, 1020), (260, 4, 1000, 36)])
+def test_pairwise_rows_off_line_boundaries(cuda, counts, argmin_path):
+    """Float32 rows that do not start on a 128-byte line (n_b % 32 != 0,
+    n_b % 4 == 0): row groups of one alignment class (stride 2, 4 or 8) and
+    chunks shifted to the line holding column 0, with masked lanes before
+    column 0 and past n_b; views of different sizes in one scene, so the
+    matrices' offsets are misaligned too, and row counts that leave the last
+    block's classes partly filled."""
+    rng = np.random.default_rng(sum(counts))
+    S, C = 2, len(counts)
+    cnt = np.array([counts, counts[::-1]], np.int64)
+    cam_offs = np.zeros(S * C + 1, np.int64)
+    np.cumsum(cnt.reshape(-1), out=cam_offs[1:])
+    pts = np.floor(rng.uniform(0, 4800, size=(cam_offs[-1], 2))) / 2
+    pairs = np.array([[a, b] for a in range(C) for b in range(C) if a != b], np.int32)
+    F = rng.normal(size=(S * len(pairs), 9))
+    F[1, [0, 1, 3, 4, 6, 7]] = 0.0      # degenerate column lines: the generic path, shifted
+    pts[int(cam_offs[1]) + 2] = [np.nan, 1.0]
+    assert_pairwise_equal(cuda, pts, cam_offs, F, pairs, S, C, options=argmin_path)
+
+
 def test_pairwise_wide_views_edge_cases(cuda, argmin_path):
     """Views of 769..1024 columns (C3's shape: several column chunks per
     wave, the lazy argmin's chunk recovery) with degenerate lines, NaN / inf / huge centroids and a column
