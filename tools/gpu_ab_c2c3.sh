@@ -6,5 +6,5 @@ tail -1 gpurun_out/abpw/parity.log
 L=bpc_baseline_amd/lib/libmvmatch_prev.so,bpc_baseline_amd/lib/libmvmatch.so
 timeout -k 10 400 python tools/ab_same_buffers.py --libs $L --workload c3 --buffers 6 --rounds 3 > gpurun_out/abpw/c3.log 2>&1 || { tail -20 gpurun_out/abpw/c3.log; exit 1; }
 tail -9 gpurun_out/abpw/c3.log
-timeout -k 10 300 python tools/ab_same_buffers.py --libs $L --workload c2 --buffers 4 --rounds 5 > gpurun_out/abpw/c2.log 2>&1 || { tail -20 gpurun_out/abpw/c2.log; exit 1; }
+timeout -k 10 300 python tools/ab_same_buffers.py --libs $L --workload c2 --buffers 4 --rounds ${C2_ROUNDS:-5} > gpurun_out/abpw/c2.log 2>&1 || { tail -20 gpurun_out/abpw/c2.log; exit 1; }
 tail -7 gpurun_out/abpw/c2.log
