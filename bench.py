@@ -15,7 +15,13 @@ detections/view x 10,000 scenes, 6 camera pairs -> 6.29e10 detection pairs
 per step.  With N GPUs the 10,000 scenes are split over the ranks (strong
 scaling, the default), so ``--gpus 8`` is configs[3]: 1,250 scenes per GPU;
 ``--scaling weak`` gives every rank its own 10,000.  Scenes are processed in
-equal launches of at most ``--chunk`` scenes; every residual is stored to HBM.
+launches of at most ``--chunk`` scenes, at least ``--min-launches`` per rank
+(5 with N > 1: the gather piece of launch k overlaps launch k+1, so only the
+last piece is exposed); every residual is stored to HBM.  At every N each
+launch of each timed step is a hipGraph captured outside the timed region and
+replayed in order, with N > 1 followed by its gather piece, so the 1 -> N
+curve compares the same launch path (``--graph steps``: one graph for all K
+steps, one GPU only; ``--graph off``: eager op calls).
 By default every launch of the timed steps writes its own output allocation
 as far as HBM holds them (C3: ten 25 GB buffers, 252 GB, one per launch of a
 step; C2: one per step), taken round robin, so a step's outputs all stay
@@ -88,14 +94,13 @@ class Chunk:
         self.row_base, self.units, self.nbytes = row_base, units, nbytes
 
 
-def build_chunks(batch, chunk, device, mode):
+def build_chunks(batch, bounds, device, mode):
     C, P = batch.n_cams, batch.n_pairs
     pts_all = torch.from_numpy(batch.pts).to(device)
     F_all = torch.from_numpy(batch.F).to(device)
     counts = batch.counts()
     chunks, row_base = [], 0
-    for s0 in range(0, batch.n_scenes, chunk):
-        s1 = min(batch.n_scenes, s0 + chunk)
+    for s0, s1 in bounds:
         co = batch.cam_offs[s0 * C:s1 * C + 1]
         base = int(co[0])
         co_rel = (co - base).astype(np.int64)
@@ -202,24 +207,44 @@ def cpu_baseline(batch, mode: str, target_s: float):
                       f"OpenMP x{threads} on {cpu_model()}"}
 
 
+def drm_card_dirs(device: torch.device):
+    """The /sys/class/drm/card*/device directory of ``device`` (matched by PCI
+    address), and a description of the match.  Falls back to every card when
+    the address cannot be matched (then the clocks are max over cards)."""
+    import glob
+    cards = sorted(glob.glob("/sys/class/drm/card[0-9]*/device"))
+    try:
+        p = torch.cuda.get_device_properties(device)
+        addr = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    except (AttributeError, RuntimeError, AssertionError):
+        addr = None
+    if addr:
+        mine = [c for c in cards if os.path.basename(os.path.realpath(c)).startswith(addr)]
+        if mine:
+            return mine, f"card of PCI {addr}"
+    return cards, "max over visible cards (PCI address not matched)"
+
+
 class ClockSampler:
     """Samples the GPU's current clock levels (the starred line of
-    /sys/class/drm/card*/device/pp_dpm_{sclk,mclk,fclk}) on a host thread while
-    the timed region runs, so run-to-run and box-to-box spread can be
-    attributed to clocks or not."""
+    /sys/class/drm/cardN/device/pp_dpm_{sclk,mclk,fclk}) of the card under
+    test on a host thread while the timed region runs, so run-to-run and
+    box-to-box spread can be attributed to clocks or not."""
 
     KINDS = ("sclk", "mclk", "fclk")
 
-    def __init__(self, period_s: float = 0.01):
+    def __init__(self, device: torch.device, period_s: float = 0.05):
         import glob
         import threading
-        self.paths = {k: sorted(glob.glob(f"/sys/class/drm/card*/device/pp_dpm_{k}"))
+        dirs, self.card_source = drm_card_dirs(device)
+        self.paths = {k: [os.path.join(d, f"pp_dpm_{k}") for d in dirs
+                          if os.path.exists(os.path.join(d, f"pp_dpm_{k}"))]
                       for k in self.KINDS}
         self.period = period_s
         self.samples = {k: [] for k in self.KINDS}
         # hwmon temperatures by label (edge / junction / mem), degrees C
         self.temp_paths = {}
-        for lab in sorted(glob.glob("/sys/class/drm/card*/device/hwmon/hwmon*/temp*_label")):
+        for lab in sorted(l for d in dirs for l in glob.glob(f"{d}/hwmon/hwmon*/temp*_label")):
             try:
                 with open(lab) as fh:
                     name = fh.read().strip()
@@ -272,7 +297,7 @@ class ClockSampler:
             self.thread.join()
 
     def temperatures(self):
-        """Max over visible cards per hwmon label, first and last sample of the
+        """Per hwmon label of the card under test, first and last sample of the
         timed region (degrees C): HBM above ~85 C refreshes twice as often."""
         out = {}
         for name, v in self.temps.items():
@@ -284,7 +309,7 @@ class ClockSampler:
         if not self.samples[kind]:
             return {"source": f"pp_dpm_{kind} unreadable", "samples": 0}
         s = np.asarray(self.samples[kind], dtype=np.float64)
-        return {"source": f"pp_dpm_{kind} (starred level, max over visible cards)",
+        return {"source": f"pp_dpm_{kind} (starred level, {self.card_source})",
                 "samples": int(s.size), "mean_mhz": float(s.mean()), "min_mhz": float(s.min()),
                 "max_mhz": float(s.max())}
 
@@ -312,14 +337,30 @@ def load_traffic(workload: str, scenes_per_launch: int):
     return rec
 
 
+def launch_bounds(n_local: int, chunk: int, min_launches: int):
+    """[(s0, s1)] scene ranges of a rank's launches: as few as keep each at
+    most ``chunk`` scenes, but at least ``min_launches`` (never more than one
+    per scene), sizes differing by at most one.  With N > 1 the association
+    gather of launch k overlaps launch k+1, so only the last launch's piece is
+    exposed: more launches per rank make that tail smaller (configs[3]: 1,250
+    scenes per rank -> 5 x 250, not 2 x 625)."""
+    from bpc_baseline_amd.distributed import shard_range
+    n_launch = max(1, -(-n_local // chunk), min(min_launches, n_local))
+    return [shard_range(n_local, k, n_launch) for k in range(n_launch)]
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
-    ap.add_argument("--scenes", type=int, default=None, help="scenes per GPU (override)")
-    ap.add_argument("--chunk", type=int, default=None, help="scenes per launch (override)")
+    ap.add_argument("--scenes", type=int, default=None, help="scenes (override; per GPU with "
+                    "--scaling weak)")
+    ap.add_argument("--chunk", type=int, default=None, help="most scenes per launch (override)")
+    ap.add_argument("--min-launches", type=int, default=None,
+                    help="fewest launches per rank and step (default: 5 with N > 1, so the "
+                         "unoverlapped last gather piece is a small part of a step; 1 on one GPU)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="strong",
                     help="strong (default): --scenes split over the GPUs, so --gpus 8 measures "
                          "BASELINE configs[3] (C3's 10k scenes, 1,250 per GPU); weak: --scenes "
@@ -333,9 +374,12 @@ def main():
     ap.add_argument("--output", choices=["resident", "ring"], default="resident",
                     help="resident (default): one output allocation per launch of the timed "
                          "steps as far as HBM holds them (reused round robin); ring: one")
-    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="replay each step's launches as one hipGraph (auto: on for a single GPU, "
-                         "where the step has no collective)")
+    ap.add_argument("--graph", choices=["launch", "steps", "off"], default="launch",
+                    help="launch (default, every N): each launch of each timed step is a hipGraph "
+                         "captured outside the timed region and replayed in order, the gather "
+                         "piece of launch k issued right after its replay; steps: one hipGraph "
+                         "holding all K steps (one GPU only: a step with N > 1 has collectives); "
+                         "off: eager op calls")
     args = ap.parse_args()
 
     wl = dict(WORKLOADS[args.workload])
@@ -349,6 +393,13 @@ def main():
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
     dev = env.device
+    if args.graph == "steps" and env.initialised:
+        raise SystemExit("--graph steps needs a single GPU without a process group "
+                         "(the step's gather is a collective)")
+    if args.scaling == "strong" and wl["n_scenes"] < world:
+        raise SystemExit(f"--scenes {wl['n_scenes']} < {world} ranks: every rank needs at least "
+                         "one scene (strong scaling splits the scenes over the ranks)")
+    min_launches = args.min_launches if args.min_launches else (5 if world > 1 else 1)
 
     # ---- this rank's shard of scenes (global scene ids are seeds) ----------
     if args.scaling == "weak":
@@ -360,10 +411,9 @@ def main():
     t0 = time.perf_counter()
     batch = make_scenes(n_local, wl["n_cams"], wl["n_dets"], seed=args.seed, first_scene=first)
     log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
-    # equal launches of at most --chunk scenes (1,250 scenes -> 2 x 625, not 1000 + 250)
-    n_launch = max(1, -(-n_local // wl["chunk"]))
-    chunk = -(-n_local // n_launch)
-    chunks, n_rows = build_chunks(batch, chunk, dev, wl["mode"])
+    bounds = launch_bounds(n_local, wl["chunk"], min_launches)
+    chunk = max(s1 - s0 for s0, s1 in bounds)    # scenes per launch (the largest)
+    chunks, n_rows = build_chunks(batch, bounds, dev, wl["mode"])
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
     max_units = max(c.units for c in chunks)
@@ -386,6 +436,7 @@ def main():
     n_slots = len(out_slots)
     seq = [0]             # launches issued (or captured) so far: the next slot
     last_slot = {}        # chunk -> the slot its latest launch wrote
+    dispatched = [0]      # kernel launches that reached the GPU (rocprof window, below)
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
 
@@ -397,6 +448,8 @@ def main():
         mv = minval[c.row_base:c.row_base + c.plan.n_rows]
         last_slot[id(c)] = seq[0] % n_slots
         seq[0] += 1
+        if not torch.cuda.is_current_stream_capturing():
+            dispatched[0] += 1
         out = out_slots[last_slot[id(c)]][:c.units]
         if wl["mode"] == "pairwise":
             ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
@@ -412,81 +465,112 @@ def main():
     except ValueError:
         gatherer, overlap = None, False
 
-    def step(events=None):
+    def eager_step():
         for k, c in enumerate(chunks):
-            if events is not None:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record(stream)
-                launch(c)
-                e1.record(stream)
-                events.append((e0, e1, c.nbytes, c.units, 1))
-            else:
-                launch(c)
+            launch(c)
             if overlap:
                 gatherer.issue(k)
-        if overlap:
-            return gatherer.finish()
-        return gather_rows(env, argmin, minval)
+        return gatherer.finish() if overlap else gather_rows(env, argmin, minval)
 
     for _ in range(args.warmup):
-        step()
+        eager_step()
     torch.cuda.synchronize(dev)
     env.barrier()
     seq[0] = 0            # the timed steps start at slot 0
 
-    # ---- single GPU: the K timed steps as ONE hipGraph (captured once,
-    # outside the timed region), so the launches of consecutive steps run back
-    # to back without the per-call host path (op dispatch, argument checks)
-    # and without a graph launch per step (~30 us, longer than a fifth of a C2
-    # kernel).  Every step still runs every launch over its whole batch.
-    graph = None
-    if args.graph == "on" or (args.graph == "auto" and not env.initialised):
-        if env.initialised:
-            raise SystemExit("--graph on needs a single GPU without a process group "
-                             "(the step's gather is a collective)")
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
+    # ---- hipGraphs, captured outside the timed region.  "launch" (every N):
+    # one graph per launch of each timed step, so the gather piece of launch k
+    # can be issued right after its replay and N = 1 and N > 1 time the same
+    # launch path; "steps" (one GPU): one graph holding all K steps.  Captured
+    # thread-locally: the RCCL watchdog thread queries events meanwhile.
+    graphs, step_graph = None, None
+    cap_kw = dict(capture_error_mode="thread_local")
+    if args.graph == "launch":
+        graphs = []
+        for _ in range(args.steps):
+            row = []
+            for c in chunks:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, **cap_kw):
+                    launch(c)
+                row.append(g)
+            graphs.append(row)
+        for row in graphs:                      # first replay uploads the graph: untimed
+            for g in row:
+                g.replay()
+                dispatched[0] += 1
+    elif args.graph == "steps":
+        step_graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(step_graph, **cap_kw):
             for _ in range(args.steps):
                 for c in chunks:
                     launch(c)
-        graph.replay()
-        torch.cuda.synchronize(dev)
-        step_bytes = sum(c.nbytes for c in chunks)
-        seq[0] = 0
+        step_graph.replay()
+        dispatched[0] += args.steps * len(chunks)
+    torch.cuda.synchronize(dev)
+    seq[0] = 0
 
-    events = []
+    def run_launch(s: int, k: int):
+        if graphs is not None:
+            graphs[s][k].replay()
+            dispatched[0] += 1
+        else:
+            launch(chunks[k])
+
+    def timed_step(s, events, tails):
+        for k, c in enumerate(chunks):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            run_launch(s, k)
+            e1.record(stream)
+            events.append((e0, e1, c.nbytes, c.units, 1))
+            if overlap:
+                gatherer.issue(k)
+        ec, es = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ec.record(stream)     # the step's compute is done here ...
+        res = gatherer.finish() if overlap else gather_rows(env, argmin, minval)
+        es.record(stream)     # ... and its association is on rank 0 here: the exposed tail
+        tails.append((ec, es))
+        return res
+
+    events, tails = [], []
     gathered = None
     torch.cuda.synchronize(dev)
     env.barrier()
-    with ClockSampler() as clocks:
+    window_start = dispatched[0]
+    with ClockSampler(dev) as clocks:
         t_start = time.perf_counter()
-        if graph is not None:   # one event pair over the timed region: no markers between steps
+        if step_graph is not None:   # one event pair over the timed region: no markers between steps
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record(stream)
-            graph.replay()      # the K steps
+            step_graph.replay()      # the K steps
             ev1.record(stream)
-            events.append((ev0, ev1, step_bytes * args.steps, units_local * args.steps,
-                           len(chunks) * args.steps))
+            dispatched[0] += args.steps * len(chunks)
+            events.append((ev0, ev1, sum(c.nbytes for c in chunks) * args.steps,
+                           units_local * args.steps, len(chunks) * args.steps))
         else:
-            for _ in range(args.steps):
-                gathered = step(events)
+            for s in range(args.steps):
+                gathered = timed_step(s, events, tails)
         torch.cuda.synchronize(dev)
         env.barrier()
         elapsed = time.perf_counter() - t_start
+    window_timed = dispatched[0] - window_start
     elapsed = max_over_ranks(env, elapsed)
+    ms_per_step = elapsed / args.steps * 1e3
 
     # ---- N > 1: the step's two parts timed apart (untimed for `value`) -----
     # compute alone (every launch, no collective) and the association gather
-    # alone, each bracketed by barrier + sync and maxed over ranks
+    # alone, each bracketed by barrier + sync and maxed over ranks; and the
+    # exposed tail of the timed steps: last launch done -> gather done
     split = None
     if env.initialised:
         reps = max(1, min(args.steps, 5))
         torch.cuda.synchronize(dev)
         env.barrier()
         t0 = time.perf_counter()
-        for _ in range(reps):
-            for c in chunks:
-                launch(c)
+        for r in range(reps):
+            for k in range(len(chunks)):
+                run_launch(r % args.steps, k)
         torch.cuda.synchronize(dev)
         env.barrier()
         t_comp = max_over_ranks(env, time.perf_counter() - t0) / reps
@@ -501,19 +585,28 @@ def main():
         torch.cuda.synchronize(dev)
         env.barrier()
         t_gath = max_over_ranks(env, time.perf_counter() - t0) / reps
+        tail_ms = float(np.mean([a.elapsed_time(b) for a, b in tails])) if tails else 0.0
+        tail_ms = max_over_ranks(env, tail_ms)
         split = {"compute_ms": t_comp * 1e3, "gather_ms": t_gath * 1e3,
                  "gather_bytes_per_rank": int(n_rows * 8),
-                 "note": "each part alone, barrier + sync around, max over ranks; in the timed "
-                         "step the gather pieces overlap the next launches"}
+                 "exposed_tail_ms": tail_ms, "exposed_tail_frac": tail_ms / ms_per_step,
+                 "note": "compute_ms / gather_ms: each part alone, barrier + sync around, max over "
+                         "ranks; exposed_tail_ms: in the timed steps, from the end of a rank's "
+                         "last launch to its gather pieces being done (HIP events on the launch "
+                         "stream, mean over steps, max over ranks) -- the part of the gather "
+                         "that no launch overlaps"}
 
     # ---- kernel roofline from the events (on the launch stream) ------------
-    # (with a graph, one event pair brackets a step's launches)
+    # (with the "steps" graph, one event pair brackets the K steps' launches)
     durs = np.array([e0.elapsed_time(e1) * 1e-3 for e0, e1, *_ in events])
     byts = np.array([b for _, _, b, _, _ in events], dtype=np.float64)
     units_ev = np.array([u for _, _, _, u, _ in events], dtype=np.float64)
     n_launch = sum(n for *_, n in events)
     avg_dur = float(durs.sum() / n_launch)
     achieved_gbs = float(byts.sum() / durs.sum() / 1e9)
+    # every rank's figure, then the slowest rank's (max launch time, min GB/s)
+    avg_dur_max = max_over_ranks(env, avg_dur)
+    achieved_min = -max_over_ranks(env, -achieved_gbs)
 
     # ---- the gathered association holds rank 0's rows first (N > 1) -------
     gather_check = None
@@ -544,7 +637,7 @@ def main():
         gd = out_of(c)[:rd.size].cpu().numpy()
         ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
         ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
-        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rd.size} pairs)"
+        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {first + s_first} ({rd.size} pairs)"
     elif env.is_root:
         from oracle import oracle as O
         c = chunks[-1]          # its cube is still in its output slot
@@ -555,7 +648,7 @@ def main():
         gc = out_of(c)[:rc.size].cpu().numpy()
         ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
         ok = np.array_equal(gc.view(np.int32), rc.view(np.int32)) and np.array_equal(ga, ra)
-        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {s_first} ({rc.size} triples)"
+        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {first + s_first} ({rc.size} triples)"
 
     # ---- PCIe-inclusive rate of one launch (never `value`) ------------------
     # the same launch fed from pinned host buffers: H2D of centroids, offsets
@@ -603,17 +696,30 @@ def main():
         torch.cuda.synchronize(dev)
         probe_gbs = 5 * n_slots * max_units * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
 
-
     units_all = sum_over_ranks(env, units_local)   # ragged shards differ by one scene
     if not env.is_root:
         return
     total_units = units_all * args.steps
     value = total_units / elapsed
     unit = "pairs/s" if wl["mode"] == "pairwise" else "triples/s"
+    # the CPU baseline runs at every N, on rank 0 after the timed region (the
+    # other ranks are done by then), on a sample of rank 0's own scenes
     cpu = None
-    if world == 1 and args.cpu_seconds > 0:
+    if args.cpu_seconds > 0:
         cpu = cpu_baseline(batch, wl["mode"], args.cpu_seconds)
+        if world > 1:
+            cpu["note"] = (f"rank 0 of {world}, after the timed region, on a sample of its own "
+                           "scenes; per host, so compare it with the whole-job value")
     traffic = load_traffic(args.workload, chunk)
+    kernel = "pairwise_kernel" if wl["mode"] == "pairwise" else "triplet_fused_kernel"
+    launch_desc = {
+        "launch": ("one hipGraph per launch of each timed step (captured once outside the timed "
+                   "region), replayed in order; with N > 1 the launch's association gather piece "
+                   "is issued right after its replay"),
+        "steps": ("one hipGraph holding the K steps' launches, captured once outside the timed "
+                  "region, replayed once"),
+        "off": "eager op calls",
+    }[args.graph]
     out = {
         "metric": METRIC if wl["mode"] == "pairwise" else "cost-cube triples/sec",
         "value": value,
@@ -621,7 +727,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
+        "ms_per_step": ms_per_step,
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,
@@ -636,8 +742,8 @@ def main():
             "output_allocations": n_slots,
             "output_gb": n_slots * max_units * 4 / 1e9,
             "units_per_gpu_step": units_local,
-            "launch": ("one hipGraph holding the K steps' launches, captured once outside the "
-                       "timed region, replayed once" if graph is not None else "eager op calls"),
+            "launch_mode": args.graph,
+            "launch": launch_desc,
             "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
                             f"({env.backend}{', overlapped per launch' if overlap else ''})")
                            if env.initialised else "single GPU",
@@ -655,21 +761,30 @@ def main():
         "temperature": clocks.temperatures(),
         "roofline": {
             "bound": "hbm",
-            "kernel": ("pairwise_kernel" if wl["mode"] == "pairwise"
-                       else "triplet_fused_kernel"),
-            "achieved": achieved_gbs,
+            "kernel": kernel,
+            "achieved": achieved_min,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "frac": achieved_min / HBM_PEAK_GBS,
             "traffic": (traffic or {}).get("bytes_per_launch"),
             "bytes_per_launch": float(byts.sum() / n_launch),
-            "avg_launch_ms": avg_dur * 1e3,
+            "avg_launch_ms": avg_dur_max * 1e3,
+            "ranks": ("slowest rank: max over ranks of the mean launch time, min over ranks of "
+                      "the achieved GB/s" if world > 1 else "one rank"),
+            "rank0": {"avg_launch_ms": avg_dur * 1e3, "achieved": achieved_gbs,
+                      "frac": achieved_gbs / HBM_PEAK_GBS},
             "event_scope": ("one event pair over the timed region (one graph replay of the K "
-                            "steps): includes the gaps between kernel nodes" if graph is not None else
-                            "one event pair per launch"),
+                            "steps): includes the gaps between kernel nodes"
+                            if step_graph is not None else "one event pair per launch"),
             "units_per_s_in_kernel": float(units_ev.sum() / durs.sum()),
             "write_probe_gbs": probe_gbs,
             "frac_of_write_probe": (achieved_gbs / probe_gbs) if probe_gbs else None,
+            # rank 0's launches of the kernel, in dispatch order: a rocprofv3
+            # kernel trace of this command holds `before` launches, then the
+            # `timed` ones this line's avg_launch_ms covers, then `after`
+            "dispatch_window": {"kernel": kernel, "before": window_start, "timed": window_timed,
+                                "after": dispatched[0] - window_start - window_timed,
+                                "slots": n_slots, "launches_per_step": len(chunks)},
         },
         "cpu_baseline": cpu,
         "pcie_inclusive": pcie,

@@ -140,14 +140,15 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
     env1 = dict(os.environ)
     for k in ("MVM_DIST_FORCE", "MVM_DIST_BACKEND", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env1.pop(k, None)
-    single = _run_bench(repo, [sys.executable, "bench.py", *common, "--graph", "off",
+    single = _run_bench(repo, [sys.executable, "bench.py", *common,
                                "--dump-association", str(tmp_path / "single")],
                         env1, tmp_path, "single")
     env2 = dict(env1, MVM_DIST_BACKEND="gloo")
     multi = _run_bench(repo, [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                               "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                               "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-                              *common, "--dump-association", str(tmp_path / "multi")],
+                              *common, "--cpu-seconds", "1",
+                              "--dump-association", str(tmp_path / "multi")],
                        env2, tmp_path, "multi")
     assert multi["n_gpus"] == 2
     assert multi["process_group"]["world_size"] == 2
@@ -156,6 +157,20 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
     assert multi["gather_check"] == "rank-0 rows equal after gather"
     assert multi["parity"].startswith("bit-exact") and single["parity"].startswith("bit-exact")
     assert multi["step_split"]["gather_ms"] > 0
+    # the N > 1 line carries what the N = 1 line does, measured the same way:
+    # the same launch path (one hipGraph per launch), a CPU baseline, and a
+    # roofline over the slowest rank next to rank 0's
+    assert single["config"]["launch_mode"] == multi["config"]["launch_mode"] == "launch"
+    assert single["config"]["launch"] == multi["config"]["launch"]
+    assert multi["cpu_baseline"] and multi["cpu_baseline"]["value"] > 0
+    assert multi["cpu_baseline"]["cores"] >= 1
+    rf = multi["roofline"]
+    assert rf["ranks"].startswith("slowest rank")
+    assert rf["avg_launch_ms"] >= rf["rank0"]["avg_launch_ms"] > 0
+    assert rf["achieved"] <= rf["rank0"]["achieved"]
+    assert 0 <= multi["step_split"]["exposed_tail_ms"]
+    assert multi["step_split"]["exposed_tail_frac"] >= 0
+    assert multi["config"]["launches_per_step"] >= min(5, n_scenes // 2)
     a1 = np.load(tmp_path / "single" / "argmin.npy")
     m1 = np.load(tmp_path / "single" / "minval.npy")
     a2 = np.load(tmp_path / "multi" / "argmin.npy")
@@ -169,11 +184,14 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("workload", ["c3", "c2cube"])
-def test_bench_graph_replay_single_gpu(tmp_path, workload):
-    """bench.py's single-GPU timed steps as one hipGraph replay: the captured
-    launches of every step run (the last launch's outputs are bit-exact vs the
-    oracle) and the per-launch event average covers every launch of every step."""
+@pytest.mark.parametrize("workload,mode", [("c3", "steps"), ("c2cube", "steps"),
+                                           ("c3", "launch"), ("c2cube", "launch")])
+def test_bench_graph_replay_single_gpu(tmp_path, workload, mode):
+    """bench.py's single-GPU timed steps as hipGraph replays (one graph for the
+    K steps, or one per launch): the captured launches of every step run (the
+    last launch's outputs are bit-exact vs the oracle), the per-launch event
+    average covers every launch of every step, and the dispatch window says
+    which of the kernel's launches a profile of the run must average."""
     import json
     import subprocess
     import sys
@@ -182,11 +200,16 @@ def test_bench_graph_replay_single_gpu(tmp_path, workload):
     env.pop("MVM_DIST_FORCE", None)
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", workload,
                         "--scenes", "24", "--chunk", "8", "--steps", "2", "--warmup", "1",
-                        "--cpu-seconds", "0", "--graph", "on"],
+                        "--cpu-seconds", "0", "--graph", mode],
                        env=env, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["parity"].startswith("bit-exact")
-    assert line["config"]["launch"].startswith("one hipGraph holding the K steps")
+    assert line["config"]["launch_mode"] == mode
+    assert line["config"]["launch"].startswith("one hipGraph holding the K steps" if mode == "steps"
+                                               else "one hipGraph per launch")
     assert line["config"]["launches_per_step"] == 3
     assert line["roofline"]["avg_launch_ms"] > 0
+    w = line["roofline"]["dispatch_window"]
+    # warmup step (3) + the untimed first replay (2 steps x 3) | 2 x 3 timed | PCIe leg (3)
+    assert (w["before"], w["timed"], w["after"]) == (3 + 6, 6, 3)

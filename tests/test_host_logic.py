@@ -365,3 +365,45 @@ def test_bench_output_slots():
     assert bench.output_slots(4 * 20, 17 * gib, 287 * gib) == 16    # the C2 cube
     assert bench.output_slots(20, gib, 287 * gib) == 20             # C2: one per step
     assert bench.output_slots(1, gib, 287 * gib) == 1
+
+
+def test_bench_launch_split():
+    """Launches of at most --chunk scenes, at least --min-launches of them,
+    sizes within one scene: configs[3] (1,250 scenes per rank) runs 5 x 250,
+    so only a fifth of a step's association gather is left unoverlapped."""
+    import bench
+
+    def sizes(n, c, m):
+        b = bench.launch_bounds(n, c, m)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(b[k][1] == b[k + 1][0] for k in range(len(b) - 1))
+        return [s1 - s0 for s0, s1 in b]
+
+    assert sizes(10000, 1000, 1) == [1000] * 10     # C3, one GPU
+    assert sizes(1250, 1000, 5) == [250] * 5         # configs[3]
+    assert sizes(5000, 1000, 5) == [1000] * 5        # two GPUs
+    assert sizes(2500, 1000, 5) == [500] * 5         # four GPUs
+    assert sizes(1000, 1000, 1) == [1000]            # C2
+    assert sizes(3, 1000, 5) == [1, 1, 1]            # fewer scenes than launches
+    assert sizes(12, 8, 5) == [3, 3, 2, 2, 2]
+    for n, c, m in ((1250, 1000, 8), (7, 2, 3), (10001, 1000, 5), (1, 1, 1)):
+        z = sizes(n, c, m)
+        assert max(z) <= c and max(z) - min(z) <= 1 and len(z) >= min(m, n)
+
+
+def test_bench_rejects_fewer_scenes_than_ranks(monkeypatch):
+    """Strong scaling with fewer scenes than ranks would leave a rank with no
+    launch while the others wait in its collectives: bench.py refuses it."""
+    import sys
+    import bench
+    from bpc_baseline_amd import distributed
+
+    class Env:
+        rank, world, local_rank, initialised, backend = 0, 8, 0, False, None
+        device = "cpu"
+
+    monkeypatch.setattr(bench, "init_from_env", lambda: Env())
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--scenes", "4"])
+    with pytest.raises(SystemExit, match="every rank needs at least one scene"):
+        bench.main()
+    assert distributed.shard_range(4, 7, 8) == (4, 4)

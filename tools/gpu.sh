@@ -1,0 +1,67 @@
+# One runner for every GPU-box task (run it through gpurun).  Chain tasks with &&.
+#
+#   bash tools/gpu.sh check [pytest args]     smoke + the -m gpu suite (one pytest process)
+#   bash tools/gpu.sh bench W [bench args]    one bench.py line of workload W
+#   bash tools/gpu.sh trace W [bench args]    the bench line under rocprofv3 --kernel-trace
+#                                             --stats (same process), reconciled with
+#                                             tools/profile_window.py
+#   bash tools/gpu.sh pmc W [bench args]      FETCH_SIZE and WRITE_SIZE, one pass each
+#   bash tools/gpu.sh sq "PMC LIST" TOOL [args]  one --pmc pass over a tools/ script
+#   bash tools/gpu.sh py TOOL [args]          a tools/ script (or bench.py) under a time limit
+#
+# Output goes to gpurun_out/$RUN/ (default gpurun_out/run).  Every GPU step has
+# its own time limit; a failing step ends the script with its status.
+set -o pipefail
+export TMPDIR=/tmp
+RUN=${RUN:-run}
+O=gpurun_out/$RUN
+mkdir -p "$O"
+LIMIT=${LIMIT:-420}
+task=$1; shift || true
+
+fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -25 "$2"; exit 1; }
+
+case "$task" in
+check)
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 \
+    || fail smoke "$O/smoke.log"
+  echo SMOKE_OK
+  timeout -k 10 1000 python -u -m pytest ${@:-tests} -x -q -m gpu --timeout 300 \
+    --timeout-method thread --durations 15 > "$O/pytest_gpu.log" 2>&1
+  rc=$?; tail -22 "$O/pytest_gpu.log"; exit $rc ;;
+bench)
+  W=$1; shift
+  timeout -k 10 "$LIMIT" python bench.py --workload "$W" "$@" > "$O/bench_$W.json" \
+    2> "$O/bench_$W.err" || fail "bench $W" "$O/bench_$W.err"
+  python tools/summarise_line.py "$O/bench_$W.json" ;;
+trace)
+  W=$1; shift
+  timeout -k 10 "$LIMIT" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_$W" \
+    -o run -- python bench.py --workload "$W" "$@" > "$O/bench_$W.json" 2> "$O/trace_$W.err" \
+    || fail "trace $W" "$O/trace_$W.err"
+  python tools/summarise_line.py "$O/bench_$W.json" &&
+  python tools/profile_window.py "$O/bench_$W.json" "$O/trace_$W/run_kernel_trace.csv" \
+    --out "$O/window_$W.json" ;;
+pmc)
+  W=$1; shift
+  for C in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${C}_$W" -o run -- \
+      python bench.py --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 "$@" \
+      > "$O/pmc_${C}_$W.log" 2>&1 || fail "pmc $C $W" "$O/pmc_${C}_$W.log"
+  done
+  echo "pmc $W ok" ;;
+sq)
+  P=$1; T=$2; shift 2
+  N=$(basename "$T" .py)
+  timeout -s KILL 200 rocprofv3 --pmc $P --output-format csv -d "$O/sq_$N" -o run -- \
+    python "$T" "$@" > "$O/sq_$N.log" 2>&1 || fail "sq $N" "$O/sq_$N.log"
+  echo "sq $N ok" ;;
+py)
+  T=$1; shift
+  N=$(basename "$T" .py)
+  timeout -k 10 "$LIMIT" python -u "$T" "$@" > "$O/$N.out" 2> "$O/$N.err" \
+    || fail "$T" "$O/$N.err"
+  tail -40 "$O/$N.out" ;;
+*)
+  echo "unknown task '$task'"; exit 2 ;;
+esac

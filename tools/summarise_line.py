@@ -1,0 +1,14 @@
+"""Print the key figures of a bench.py JSON line: python tools/summarise_line.py LINE.json"""
+import json
+import sys
+
+with open(sys.argv[1]) as fh:
+    d = json.loads([l for l in fh if l.lstrip().startswith("{")][-1])
+r = d["roofline"]
+cpu = d.get("cpu_baseline") or {}
+sp = d.get("step_split") or {}
+print(f"{d['config'].get('launch_mode')} N={d['n_gpus']} value {d['value']:.4g} {d['unit']} "
+      f"ms/step {d['ms_per_step']:.3f} launch {r['avg_launch_ms']:.4f} ms frac {r['frac']:.4f} "
+      f"probe {r.get('write_probe_gbs') or 0:.0f} GB/s of-probe {r.get('frac_of_write_probe') or 0:.3f} "
+      f"sclk {d['sclk'].get('mean_mhz', 0):.0f} cpu {cpu.get('value', 0):.3g} "
+      f"tail {sp.get('exposed_tail_ms', 0):.3f} ms | {d['parity']}")
