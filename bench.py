@@ -88,10 +88,11 @@ def cube_bytes(counts: np.ndarray) -> float:
 
 
 class Chunk:
-    def __init__(self, s0, pts, cam_offs, F, plan, row_base, units, nbytes):
+    def __init__(self, s0, pts, cam_offs, F, plan, row_base, units, size, nbytes):
         self.s0 = s0
         self.pts, self.cam_offs, self.F, self.plan = pts, cam_offs, F, plan
         self.row_base, self.units, self.nbytes = row_base, units, nbytes
+        self.size = size          # output floats (>= units when rows are pitched)
 
 
 def build_chunks(batch, bounds, device, mode):
@@ -108,14 +109,14 @@ def build_chunks(batch, bounds, device, mode):
         F = F_all[s0 * P:s1 * P]
         if mode == "pairwise":
             plan = ops.PairwisePlan(co_rel, s1 - s0, C, batch.pairs, device=device)
-            units = int(plan.n_dist)
+            units, size = int(plan.n_dist), int(plan.dist_size)
             nbytes = pairwise_bytes(counts[s0:s1], batch.pairs)
         else:
             plan = ops.TripletPlan(co_rel, s1 - s0, device=device)
-            units = int(plan.n_cube)
+            units = size = int(plan.n_cube)
             nbytes = cube_bytes(counts[s0:s1])
         chunks.append(Chunk(s0, pts, torch.from_numpy(co_rel).to(device), F, plan, row_base, units,
-                            nbytes))
+                            size, nbytes))
         row_base += plan.n_rows
     return chunks, row_base
 
@@ -416,7 +417,7 @@ def main():
     chunks, n_rows = build_chunks(batch, bounds, dev, wl["mode"])
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
-    max_units = max(c.units for c in chunks)
+    max_units = max(c.size for c in chunks)
     # output slots: one allocation per launch of the timed steps when they fit
     # (a step's residuals all stay resident, and consecutive steps write other
     # allocations, as a service that double-buffers its outputs would),
@@ -441,7 +442,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     def out_of(c: Chunk):
-        return out_slots[last_slot[id(c)]][:c.units]
+        """The chunk's residuals in the unpitched layout."""
+        out = out_slots[last_slot[id(c)]][:c.size]
+        return c.plan.compact(out) if wl["mode"] == "pairwise" else out
 
     def launch(c: Chunk):
         am = argmin[c.row_base:c.row_base + c.plan.n_rows]
@@ -450,7 +453,7 @@ def main():
         seq[0] += 1
         if not torch.cuda.is_current_stream_capturing():
             dispatched[0] += 1
-        out = out_slots[last_slot[id(c)]][:c.units]
+        out = out_slots[last_slot[id(c)]][:c.size]
         if wl["mode"] == "pairwise":
             ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
         else:

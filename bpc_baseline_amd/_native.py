@@ -87,6 +87,11 @@ SIGNATURES = {
         _i32, _i32, _i32, _i32,
         _vp, _vp, _vp, _vp, _vp,
         _vp, _vp]),                         # options (host), stream
+    "mvm_pairwise_residual_argmin_pitched": (ctypes.c_int, [
+        _vp, _vp, _vp, _vp, _vp,
+        _i32, _i32, _i32, _i32, _i32,       # n_scenes, n_cams, n_pairs, max_n, row_align
+        _vp, _vp, _vp, _vp, _vp,
+        _vp, _vp]),                         # options (host), stream
     "mvm_pairwise_residual_f64": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp,
         _i32, _i32, _i32, _i32,

@@ -43,12 +43,13 @@ struct PairArgs {
     int32_t *argmin;
     float *minval;
     int64_t mat_stride;
-    int64_t ld;                 // row stride of each matrix; 0 -> n_b
+    int64_t ld;                 // row stride of each matrix; 0 -> n_b rounded up to row_align
+    int32_t row_align;          // >= 1: rows start every roundup(n_b, row_align) floats
     int32_t n_cams, n_pairs, row_blocks;
     int32_t rows_per_wg;        // kWaves * RPW * row groups
     int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
-    int32_t lazy;               // clean row groups: 2 lazy argmin + transposed reduction,
-                                // 1 lazy + per-row reductions, 0 eager (mvm_options)
+    int32_t lazy;               // clean row groups: 1 lazy argmin + transposed reduction,
+                                // 0 eager (mvm_options)
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -60,11 +61,14 @@ struct ColRegs {
 };
 // One row x 4 columns of one lane, clean case: 7 fp64 ops + 1 int op + 1 cvt
 // per pair, one 16-byte store, 3 int ops of argmin per pair.
-// MASK: the tail chunk of an aligned matrix (n_b % 4 == 0): a lane's 4 columns
-// are all in the view or all past it (state kNone), and only the former store.
+// MASK: the tail chunk of an aligned matrix: a lane's 4 columns are all in the
+// row's pitch or all past it (jbase >= lim), and only the former store
+// (padding columns between n_b and the pitch hold +inf: their lines are the
+// pad lines of load_tile, and +inf never wins the argmin).
 template <bool ARGMIN, bool STORE, typename OutT, int NT = 1, bool MASK = false>
 __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl1, double rl2,
-                                         double rx, double ry, OutT *drow, int jbase, Best &best) {
+                                         double rx, double ry, OutT *drow, int jbase, Best &best,
+                                         int lim = 0) {
     double e[kColsPerLane];
     float v[kColsPerLane];
 #pragma unroll
@@ -79,7 +83,7 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
         }
     }
     if constexpr (sizeof(OutT) == 4) {
-        if (MASK && c.state[0] == kNone) return;
+        if (MASK && jbase >= lim) return;
         if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
         if (ARGMIN) {
 #pragma unroll
@@ -135,13 +139,12 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
 // ---- lazy argmin (clean row groups) ----
 // In a row group whose rows and columns are all clean (finite, non-degenerate,
 // one column tile), a lane keeps per row only the float32 bits of its minimum
-// (non-negative finite floats order like their bits) and the CHUNK it came
-// from: two v_min3_u32 + one compare + one select per 4 pairs instead of a
-// compare and two selects per pair.  The column inside the chunk is recovered
-// once per group (lane r recomputes the 4 values of row r's winning lane and
-// chunk, `lazy_recover`), so the result is exactly np.argmin's: the earliest
-// chunk wins inside a lane (strict '<'), the lowest q inside a chunk, and
-// rows whose minimum sits in several lanes take the tie path.
+// (non-negative finite floats order like their bits): two v_min3_u32 per 4
+// pairs instead of a compare and two selects per pair.  The winning column is
+// recovered once per group (the row slot's lanes recompute the winning lane's
+// values in every chunk and keep the first equal to the minimum), so the
+// result is exactly np.argmin's lowest-index rule; rows whose minimum sits in
+// several lanes over several chunks take the tie path.
 
 // float32 bits of the 4 stored values of one lane for one row (row_fast's arithmetic)
 __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double rl1, double rl2,
@@ -154,20 +157,18 @@ __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double 
     }
 }
 
-// TRACK: also keep the chunk of the minimum (lazy == 1); lazy == 2 keeps the
-// bits only (two v_min3_u32 per 4 pairs) and recovers the chunk at group end
-template <bool STORE, int NT, bool TRACK>
+// Lazy argmin: per row a lane keeps only the float32 bits of its minimum over
+// the chunks it has seen -- two v_min3_u32 per 4 pairs; the column is
+// recovered at the end of the row group (lazy_reduce_bits + recovery below)
+template <bool STORE, int NT>
 __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
                                               double rx, double ry, float *drow, int jbase,
-                                              uint32_t &bbits, int32_t &bchunk, int32_t cidx) {
+                                              uint32_t &bbits) {
     float v[kColsPerLane];
     pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
     if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
-    const uint32_t m = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]),
-                                         __float_as_uint(v[2])),
-                                __float_as_uint(v[3]), bbits);
-    if (TRACK) bchunk = (m < bbits) ? cidx : bchunk;
-    bbits = m;
+    bbits = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2])),
+                     __float_as_uint(v[3]), bbits);
 }
 
 // float32 bits of the stored value of column jj (tile-local) against row slot
@@ -180,30 +181,7 @@ __device__ __forceinline__ uint32_t pair_bits1(const double *s_l0, const double 
     return __float_as_uint((float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2)));
 }
 
-// Column (within the tile) of the first of the 4 values of columns jj0..jj0+3
-// against row line/point `rl`/`rx,ry` whose bits equal `k` (4 if none).
-__device__ __forceinline__ int lazy_first_q(const double *s_l0, const double *s_l1,
-                                            const double *s_l2, const double *s_x,
-                                            const double *s_y, int jj0, double rl0, double rl1,
-                                            double rl2, double rx, double ry, uint32_t k) {
-    ColRegs c;
-#pragma unroll
-    for (int q = 0; q < kColsPerLane; ++q) {
-        c.l0[q] = s_l0[jj0 + q];
-        c.l1[q] = s_l1[jj0 + q];
-        c.l2[q] = s_l2[jj0 + q];
-        c.x[q] = s_x[jj0 + q];
-        c.y[q] = s_y[jj0 + q];
-    }
-    float v[kColsPerLane];
-    pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
-    int q = kColsPerLane;
-#pragma unroll
-    for (int p = kColsPerLane - 1; p >= 0; --p) q = (__float_as_uint(v[p]) == k) ? p : q;
-    return q;
-}
-
-// ---- transposed lazy reduction (lazy == 2, the default) ----
+// ---- transposed lazy reduction (the default) ----
 // Minimum over the LPR = 64 / RPW consecutive lanes that share one row slot.
 // Quad xor steps, then row_half_mirror / row_mirror: every lane of the group
 // ends with the group minimum.
@@ -233,54 +211,11 @@ __device__ __forceinline__ void read_segment(const uint32_t *red, int rs, int se
     }
 }
 
-// End of a clean (lazy) row group.  Lane L holds, per row slot r, the float32
-// bits of its minimum bbits[r] and the chunk it first reached it in,
-// bchunk[r].  The per-row wave reductions (RPW x (4 DPP + 4 readlane + ballot
-// + selects)) become one transpose through LDS: lane L takes row slot
-// rs = L / LPR and the RPW lanes [seg*RPW, seg*RPW + RPW) of that row
-// (seg = L % LPR), reduces them in registers, and finishes over its LPR lanes
-// with DPP.  The winner is the lowest (chunk, lane) holding the row minimum k
-// -- the lowest column, since column = chunk*256 + 4*lane + q.  Returns k and
-// the winner's lane and chunk, uniform over the LPR lanes of the row slot.
-template <int RPW>
-__device__ __forceinline__ void lazy_reduce_transposed(uint32_t *red, const uint32_t (&bbits)[RPW],
-                                                       const int32_t (&bchunk)[RPW], bool multi,
-                                                       int lane, uint32_t &k, int &w, int &c) {
-    constexpr int LPR = kWave / RPW;
-    const int rs = lane / LPR, seg = lane % LPR;
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = bbits[r];
-    // the same wave reads them back: LDS executes one wave's ops in order
-    uint32_t v[RPW];
-    read_segment<RPW>(red, rs, seg, v);
-    uint32_t m = v[0];
-#pragma unroll
-    for (int i = 1; i < RPW; ++i) m = v[i] < m ? v[i] : m;
-    k = group_min_u32<RPW>(m);
-    uint32_t key = 0xFFFFFFFFu;
-    if (!multi) {   // one chunk: the first lane of the segment holding k
-        uint32_t pos = RPW;
-#pragma unroll
-        for (int i = RPW - 1; i >= 0; --i) pos = (v[i] == k) ? (uint32_t)i : pos;
-        key = (pos < (uint32_t)RPW) ? (uint32_t)(seg * RPW) + pos : key;
-    } else {        // several chunks: lowest (chunk, lane) among the lanes holding k
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) red[r * kWave + lane] = (uint32_t)bchunk[r];
-        uint32_t ch[RPW];
-        read_segment<RPW>(red, rs, seg, ch);
-#pragma unroll
-        for (int i = 0; i < RPW; ++i) {
-            const uint32_t ki = (ch[i] << 6) | (uint32_t)(seg * RPW + i);
-            const uint32_t cand = (v[i] == k) ? ki : 0xFFFFFFFFu;
-            key = cand < key ? cand : key;
-        }
-    }
-    key = group_min_u32<RPW>(key);
-    w = (int)(key & 63u);
-    c = (int)(key >> 6);
-}
-
-// lazy == 2: the same transpose without chunks.  Returns the row minimum k,
+// End of a clean (lazy) row group.  Lane L holds, per row slot r, the
+// float32 bits of its minimum bbits[r].  One transpose through LDS: lane L
+// takes row slot rs = L / LPR and the RPW lanes [seg*RPW, seg*RPW + RPW) of
+// that row (seg = L % LPR), reduces them in registers, and finishes over its
+// LPR lanes with DPP.  Returns the row minimum k,
 // the lowest lane w holding it, and whether another lane holds it too (`tie`:
 // with several chunks the lowest lane is then not necessarily the lowest
 // column).  Uniform over the LPR lanes of a row slot.
@@ -333,7 +268,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
     double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
     double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
     uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
-    // lazy == 2: per wave an [RPW][64] u32 scratch for the transposed reduction
+    // lazy argmin: per wave an [RPW][64] u32 scratch for the transposed reduction
     uint32_t *s_red = s_cst + T;
 
     const int t = threadIdx.x;
@@ -369,7 +304,10 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
     // first association row of this matrix, loaded before any store (a vector
     // load issued after the stores would wait for all of them: vmcnt is in order)
     const int64_t row_off0 = args.row_offs ? args.row_offs[sp] : 0;
-    const int64_t ld = args.ld ? args.ld : nb;
+    const int ra = args.row_align > 1 ? args.row_align : 1;
+    const int64_t ld = args.ld ? args.ld : (int64_t)((nb + ra - 1) / ra) * ra;
+    // columns a row stores: its padding too when pitched, so whole lines go out
+    const int lim = (int)min(ld, (int64_t)0x7FFFFFFF);
     OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
     const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
     // unaligned float32 rows: lanes take strided columns (coalesced dword stores)
@@ -379,8 +317,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
     auto load_tile = [&](int c0) {
         for (int jj = t; jj < T; jj += kThreads) {
             const int j = c0 + jj;
+            // past the view: a pad line, whose pair values are +inf (l1.p1 = +inf,
+            // l2.p2 = rl2 finite) -- never a row minimum, and what a pitched
+            // row's padding holds
             uint32_t st = kNone;
-            double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+            double l0 = 0, l1 = 0, l2 = __builtin_inf(), x = 0, y = 0;
             if (j < nb) {
                 x = args.pts[2 * (ob + j)];
                 y = args.pts[2 * (ob + j) + 1];
@@ -405,9 +346,10 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
     const int n_tiles = (nb + T - 1) / T;
     if (n_tiles == 1) load_tile(0);
     // lazy argmin needs every column of the (single) tile clean
-    bool my_clean = n_tiles == 1;
+    // (padding columns are pad lines: clean for the lazy argmin)
+    bool my_clean = n_tiles == 1 && nb > 0;
     if (ARGMIN && sizeof(OutT) == 4 && args.lazy && n_tiles == 1)
-        for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] == kOk);
+        for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] != kDeg && s_cst[jj] != kWild);
     const bool tile_clean = __syncthreads_and(my_clean) != 0;
 
     const int n_groups = (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
@@ -460,152 +402,97 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                           tile_clean && rows_fast && (vec_ok || !dbase);
         if (lazy) {
             uint32_t bbits[RPW];
-            int32_t bchunk[RPW];
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                bbits[r] = 0x7F800000u;
-                bchunk[r] = 0;
-            }
-            auto sweep = [&](auto track) {
-                constexpr bool TRACK = decltype(track)::value;
-                for (int c0 = 0, cidx = 0; c0 < nb; c0 += kChunk, ++cidx) {
-                    ColRegs c;
+            for (int r = 0; r < RPW; ++r) bbits[r] = 0x7F800000u;
+            for (int c0 = 0; c0 < nb; c0 += kChunk) {
+                const int jbase = c0 + kColsPerLane * lane;
+                // the last chunk of a ragged view: lanes past the row's pitch
+                // sit out (their columns hold pad lines: +inf, never a minimum)
+                if (jbase >= lim) continue;
+                ColRegs c;
 #pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) {
-                        const int jj = c0 + kColsPerLane * lane + q;
-                        c.l0[q] = s_l0[jj];
-                        c.l1[q] = s_l1[jj];
-                        c.l2[q] = s_l2[jj];
-                        c.x[q] = s_x[jj];
-                        c.y[q] = s_y[jj];
-                    }
-                    const int jbase = c0 + kColsPerLane * lane;
-                    if (dbase) {
-                        const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
-                        uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
-#pragma unroll
-                        for (int r = 0; r < RPW; ++r) {
-                            row_fast_lazy<true, NT, TRACK>(c, rowp[r][0], rowp[r][1],
-                                                           rowp[r][2], rowp[r][3],
-                                                           rowp[r][4], reinterpret_cast<float *>(rp),
-                                                           jbase, bbits[r], bchunk[r], cidx);
-                            rp += rstep;
-                            // keep the row address a running scalar: stops LICM
-                            // hoisting all RPW row bases out of the chunk loop
-                            // (they would be spilled to VGPR lanes)
-                            __asm__ volatile("" : "+s"(rp));
-                        }
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < RPW; ++r)
-                            row_fast_lazy<false, NT, TRACK>(c, rowp[r][0], rowp[r][1],
-                                                            rowp[r][2], rowp[r][3],
-                                                            rowp[r][4], nullptr, jbase, bbits[r],
-                                                            bchunk[r], cidx);
-                    }
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = jbase + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
                 }
-            };
-            if (args.lazy >= 2) {
-                sweep(std::false_type{});
-                constexpr int LPR = kWave / RPW;
-                constexpr int VPL = kColsPerLane * (kMaxColTile / kChunk) / LPR;
-                static_assert(VPL >= 1 && LPR * VPL == kColsPerLane * (kMaxColTile / kChunk),
-                              "recovery slots");
-                // the lane id as a fresh value per group: everything derived
-                // from it here (row slot, LDS and output addresses) is then
-                // recomputed per group instead of hoisted out of the group loop
-                // and spilled -- at 3 waves/SIMD (C2) those spills were reloaded
-                // after the group's stores, and the in-order vmcnt wait for the
-                // reload drained all of them
-                int lz = lane;
-                __asm__ volatile("" : "+v"(lz));
-                uint32_t k;
-                int w;
-                bool tie;
-                lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lz, k, w, tie);
-                // the LPR lanes of row slot rs recompute lane w's values in
-                // every chunk (slot idx = chunk * 4 + q; lazy tiles have
-                // nb == T, a multiple of kChunk) and keep the first equal to k
-                const int rs = lz / LPR, seg = lz % LPR;
-                const int n_ch = nb / kChunk;
-                const double *rl = rowp[rs];
-                uint32_t first = 0xFFFFFFFFu;
+                if (dbase) {
+                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
+                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
 #pragma unroll
-                for (int t = VPL - 1; t >= 0; --t) {
-                    const int idx = seg + LPR * t;
-                    const int c = idx / kColsPerLane, q = idx % kColsPerLane;
-                    if (c < n_ch) {
-                        const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
-                                                      c * kChunk + kColsPerLane * w + q, rl);
-                        first = (b == k) ? (uint32_t)idx : first;
+                    for (int r = 0; r < RPW; ++r) {
+                        row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1], rowp[r][2],
+                                                rowp[r][3], rowp[r][4],
+                                                reinterpret_cast<float *>(rp), jbase, bbits[r]);
+                        rp += rstep;
+                        // keep the row address a running scalar: stops LICM
+                        // hoisting all RPW row bases out of the chunk loop
+                        // (they would be spilled to VGPR lanes)
+                        __asm__ volatile("" : "+s"(rp));
                     }
-                }
-                first = group_min_u32<RPW>(first);
-                int jwin = (int)(first / kColsPerLane) * kChunk + kColsPerLane * w +
-                           (int)(first % kColsPerLane);
-                // rare: several lanes hold the minimum over several chunks ->
-                // the row slot's lanes scan every column for the first equal to k
-                tie = tie && n_ch > 1;
-                if (__builtin_expect(__any(tie), 0)) {
-                    if (tie) {
-                        uint32_t jt = 0xFFFFFFFFu;
-                        for (int jj = nb - LPR + seg; jj >= 0; jj -= LPR)
-                            jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj, rl) == k)
-                                     ? (uint32_t)jj : jt;
-                        jwin = (int)group_min_u32<RPW>(jt);
-                    }
-                }
-                if (seg == 0) {
-                    const int64_t row = row_off0 + grow0 + rs;
-                    if (args.argmin) args.argmin[row] = jwin;
-                    if (args.minval) args.minval[row] = __uint_as_float(k);
-                }
-                continue;
-            }
-            sweep(std::true_type{});
-            // per row: wave minimum, its lane and chunk; lane r gathers row r's
-            uint32_t my_k = 0;
-            int32_t my_l = 0, my_c = 0;
-            uint32_t ties = 0;   // rows whose minimum sits in several lanes
+                } else {
 #pragma unroll
-            for (int r = 0; r < RPW; ++r) {
-                const uint32_t k = wave_min_u32(bbits[r]);
-                const uint64_t hit = __ballot(bbits[r] == k);
-                const int wl = (int)__builtin_ctzll(hit);
-                ties |= (__builtin_popcountll(hit) > 1) ? (1u << r) : 0u;
-                const int wc = __builtin_amdgcn_readlane(bchunk[r], wl);
-                my_k = (lane == r) ? k : my_k;
-                my_l = (lane == r) ? wl : my_l;
-                my_c = (lane == r) ? wc : my_c;
-            }
-            int32_t my_j = 0;
-            if (lane < RPW) {   // lane r recovers the column of row slot r
-                const int jj0 = my_c * kChunk + kColsPerLane * my_l;
-                my_j = jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0, rowp[lane][0],
-                                          rowp[lane][1], rowp[lane][2],
-                                          rowp[lane][3], rowp[lane][4], my_k);
-            }
-            if (ties) {
-#pragma unroll
-                for (int r = 0; r < RPW; ++r) {
-                    if (!(ties & (1u << r))) continue;   // uniform
-                    const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)my_k, r);
-                    uint32_t cand = 0x7FFFFFFFu;
-                    if (bbits[r] == k) {   // every lane holding the minimum finds its first column
-                        const int jj0 = bchunk[r] * kChunk + kColsPerLane * lane;
-                        cand = (uint32_t)(jj0 + lazy_first_q(s_l0, s_l1, s_l2, s_x, s_y, jj0,
-                                                             rowp[r][0], rowp[r][1],
-                                                             rowp[r][2], rowp[r][3],
-                                                             rowp[r][4], k));
-                    }
-                    const int32_t jt = (int32_t)wave_min_u32(cand);
-                    my_j = (lane == r) ? jt : my_j;
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast_lazy<false, NT>(c, rowp[r][0], rowp[r][1], rowp[r][2],
+                                                 rowp[r][3], rowp[r][4], nullptr, jbase,
+                                                 bbits[r]);
                 }
             }
-            if (lane < nrows) {
-                const int64_t row = row_off0 + grow0 + lane;
-                if (args.argmin) args.argmin[row] = my_j;
-                if (args.minval) args.minval[row] = __uint_as_float(my_k);
+            constexpr int LPR = kWave / RPW;
+            constexpr int VPL = kColsPerLane * (kMaxColTile / kChunk) / LPR;
+            static_assert(VPL >= 1 && LPR * VPL == kColsPerLane * (kMaxColTile / kChunk),
+                          "recovery slots");
+            // the lane id as a fresh value per group: everything derived
+            // from it here (row slot, LDS and output addresses) is then
+            // recomputed per group instead of hoisted out of the group loop
+            // and spilled -- at 3 waves/SIMD (C2) those spills were reloaded
+            // after the group's stores, and the in-order vmcnt wait for the
+            // reload drained all of them
+            int lz = lane;
+            __asm__ volatile("" : "+v"(lz));
+            uint32_t k;
+            int w;
+            bool tie;
+            lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lz, k, w, tie);
+            // the LPR lanes of row slot rs recompute lane w's values in
+            // every chunk (slot idx = chunk * 4 + q; lazy tiles have
+            // nb == T, a multiple of kChunk) and keep the first equal to k
+            const int rs = lz / LPR, seg = lz % LPR;
+            const int n_ch = (nb + kChunk - 1) / kChunk;
+            const double *rl = rowp[rs];
+            uint32_t first = 0xFFFFFFFFu;
+#pragma unroll
+            for (int t = VPL - 1; t >= 0; --t) {
+                const int idx = seg + LPR * t;
+                const int c = idx / kColsPerLane, q = idx % kColsPerLane;
+                if (c < n_ch) {
+                    const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
+                                                  c * kChunk + kColsPerLane * w + q, rl);
+                    first = (b == k) ? (uint32_t)idx : first;
+                }
+            }
+            first = group_min_u32<RPW>(first);
+            int jwin = (int)(first / kColsPerLane) * kChunk + kColsPerLane * w +
+                       (int)(first % kColsPerLane);
+            // rare: several lanes hold the minimum over several chunks ->
+            // the row slot's lanes scan every column for the first equal to k
+            tie = tie && n_ch > 1;
+            if (__builtin_expect(__any(tie), 0)) {
+                if (tie) {
+                    uint32_t jt = 0xFFFFFFFFu;
+                    for (int jj = nb - LPR + seg; jj >= 0; jj -= LPR)
+                        jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj, rl) == k)
+                                 ? (uint32_t)jj : jt;
+                    jwin = (int)group_min_u32<RPW>(jt);
+                }
+            }
+            if (seg == 0) {
+                const int64_t row = row_off0 + grow0 + rs;
+                if (args.argmin) args.argmin[row] = jwin;
+                if (args.minval) args.minval[row] = __uint_as_float(k);
             }
             continue;
         }
@@ -658,7 +545,8 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                         row_fast<ARGMIN, true, OutT, NT, true>(
                             c, rowp[r][0], rowp[r][1], rowp[r][2],
                             rowp[r][3], rowp[r][4],
-                            reinterpret_cast<OutT *>(rbase + (uint64_t)r * rstep), jbase, best[r]);
+                            reinterpret_cast<OutT *>(rbase + (uint64_t)r * rstep), jbase, best[r],
+                            lim);
                     }
                 } else if (fast && vec_ok) {   // the common case: clean rows, aligned output
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
@@ -765,11 +653,12 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
-    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, argmin && !f64 && a.lazy >= 2);
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, argmin && !f64 && a.lazy);
     if (f64) return launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
-    // nontemporal stores for whole-line rows; rows that end mid-line share
-    // that line with the next row, and L2 must merge it (default policy)
-    if (max_cols % 32 == 0) {
+    // nontemporal stores for whole-line rows (views of a multiple of 32, or
+    // rows pitched to 128-byte lines); rows that end mid-line share that line
+    // with the next row, and L2 must merge it (default policy)
+    if (max_cols % 32 == 0 || a.row_align % 32 == 0) {
         // LDS allows at most two workgroups per CU (> 160 KiB / 3; C3's 1,024
         // column lines): the register cap of three waves per SIMD buys nothing
         // there, and at 168 VGPRs the kernel spills -- a scratch reload ahead
@@ -794,8 +683,8 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     if (n_scenes == 0 || max_rows == 0) return MVM_OK;
     switch (o.pairwise_argmin) {
     case MVM_PAIRWISE_ARGMIN_DEFAULT:
-    case MVM_PAIRWISE_ARGMIN_LAZY_TRANSPOSED: a.lazy = 2; break;
-    case MVM_PAIRWISE_ARGMIN_LAZY_ROWS: a.lazy = 1; break;
+    case MVM_PAIRWISE_ARGMIN_LAZY_TRANSPOSED:
+    case MVM_PAIRWISE_ARGMIN_LAZY_ROWS: a.lazy = 1; break;   // LAZY_ROWS: an alias since ABI 3
     case MVM_PAIRWISE_ARGMIN_EAGER: a.lazy = 0; break;
     default: return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_argmin %d", (int)o.pairwise_argmin);
     }
@@ -841,17 +730,20 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
 // ================================================================ C ABI ====
 extern "C" {
 
-int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
-                                    const double *F_dev, const int32_t *pair_a,
-                                    const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
-                                    int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
-                                    const int64_t *row_offs_dev, float *dist_dev,
-                                    int32_t *argmin_dev, float *minval_dev,
-                                    const mvm_options *opts, mvm_stream_t stream) {
+int mvm_pairwise_residual_argmin_pitched(const double *pts_dev, const int64_t *cam_offs_dev,
+                                         const double *F_dev, const int32_t *pair_a,
+                                         const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                         int32_t n_pairs, int32_t max_n, int32_t row_align,
+                                         const int64_t *dist_offs_dev, const int64_t *row_offs_dev,
+                                         float *dist_dev, int32_t *argmin_dev, float *minval_dev,
+                                         const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
     mvm_options o;
     int st = mvm_resolve_options(opts, o);
     if (st) return st;
+    if (row_align < 1 || row_align > 256 || (row_align & (row_align - 1)))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "row_align %d not a power of two in [1, 256]",
+                        (int)row_align);
     PairArgs a{};
     st = fill_pairs(a, pair_a, pair_b, n_pairs, n_cams);
     if (st) return st;
@@ -869,9 +761,23 @@ int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_of
     a.argmin = argmin_dev;
     a.minval = minval_dev;
     a.ld = 0;
+    a.row_align = row_align;
     const bool want_argmin = argmin_dev || minval_dev;
     return launch_pairwise_common(a, n_scenes, max_n, max_n, want_argmin, false, o,
                                   reinterpret_cast<hipStream_t>(stream));
+}
+
+int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
+                                    const double *F_dev, const int32_t *pair_a,
+                                    const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                    int32_t n_pairs, int32_t max_n, const int64_t *dist_offs_dev,
+                                    const int64_t *row_offs_dev, float *dist_dev,
+                                    int32_t *argmin_dev, float *minval_dev,
+                                    const mvm_options *opts, mvm_stream_t stream) {
+    return mvm_pairwise_residual_argmin_pitched(pts_dev, cam_offs_dev, F_dev, pair_a, pair_b,
+                                                n_scenes, n_cams, n_pairs, max_n, 1, dist_offs_dev,
+                                                row_offs_dev, dist_dev, argmin_dev, minval_dev,
+                                                opts, stream);
 }
 
 int mvm_pairwise_residual_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
@@ -904,6 +810,7 @@ int mvm_pairwise_residual_f64(const double *pts_dev, const int64_t *cam_offs_dev
     a.dist = e_dev;
     a.mat_stride = mat_stride;
     a.ld = ld;
+    a.row_align = 1;
     mvm_options o;
     mvm_options_init(&o);
     return launch_pairwise_common(a, n_scenes, max_n, max_n, false, true, o,

@@ -112,7 +112,7 @@ def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_
                                  pair_b: List[int], n_scenes: int, n_cams: int, max_n: int,
                                  dist_offs: Tensor, row_offs: Tensor, dist: Tensor,
                                  argmin: Tensor, minval: Tensor,
-                                 opts: Optional[List[int]] = None) -> None:
+                                 opts: Optional[List[int]] = None, row_align: int = 1) -> None:
     n_pairs = len(pair_a)
     _check_inputs(pts, cam_offs, F, n_scenes * n_cams, n_scenes * n_pairs)
     for t, n, dt in ((dist_offs, "dist_offs", torch.int64), (row_offs, "row_offs", torch.int64),
@@ -121,16 +121,16 @@ def pairwise_residual_argmin_out(pts: Tensor, cam_offs: Tensor, F: Tensor, pair_
         _require(t, n, dt, pts.device)
     pa = (ctypes.c_int32 * n_pairs)(*pair_a)
     pb = (ctypes.c_int32 * n_pairs)(*pair_b)
-    st = _native.load().mvm_pairwise_residual_argmin_ex(
-        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_n,
+    st = _native.load().mvm_pairwise_residual_argmin_pitched(
+        _p(pts), _p(cam_offs), _p(F), pa, pb, n_scenes, n_cams, n_pairs, max_n, row_align,
         _p(dist_offs), _p(row_offs), _p(dist), _p(argmin), _p(minval), _opts_ref(opts),
         _stream(pts))
-    _native.check("mvm_pairwise_residual_argmin_ex", st)
+    _native.check("mvm_pairwise_residual_argmin_pitched", st)
 
 
 @pairwise_residual_argmin_out.register_fake
 def _(pts, cam_offs, F, pair_a, pair_b, n_scenes, n_cams, max_n, dist_offs, row_offs, dist,
-      argmin, minval, opts=None):
+      argmin, minval, opts=None, row_align=1):
     return None
 
 
@@ -323,18 +323,33 @@ class PairwisePlan:
 
     Built on the host from ``cam_offs`` (the per-view counts are host
     knowledge: they come from the detector), copied once to ``device``.
+
+    ``row_align``: rows of matrix (s, p) are ``ld = roundup(n_b, row_align)``
+    floats apart (include/mvmatch.h, mvm_pairwise_residual_argmin_pitched).
+    "auto" (the default) pitches rows to 128-byte lines (32 floats) when some
+    view's count is not a multiple of 32 -- the ragged views real detectors
+    produce, whose unpitched rows would start mid-line -- and keeps the
+    unpitched layout otherwise (then the two are the same).  ``matrix()``
+    returns the (n_a, n_b) view of a matrix either way; ``compact()`` the
+    unpitched flat layout.
     """
 
     def __init__(self, cam_offs: np.ndarray, n_scenes: int, n_cams: int, pairs,
-                 device: torch.device | str = "cuda"):
+                 device: torch.device | str = "cuda", row_align="auto"):
         cam_offs = np.asarray(cam_offs, dtype=np.int64)
         pairs = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
         counts = np.diff(cam_offs).reshape(n_scenes, n_cams)
         na = counts[:, pairs[:, 0]].reshape(-1)
         nb = counts[:, pairs[:, 1]].reshape(-1)
+        if row_align == "auto":
+            row_align = 32 if (nb % 32).any() else 1
+        row_align = int(row_align)
+        if row_align < 1 or row_align > 256 or row_align & (row_align - 1):
+            raise ValueError(f"row_align {row_align}: a power of two in [1, 256]")
+        ld = (nb + row_align - 1) // row_align * row_align
         dist_offs = np.zeros(na.size + 1, np.int64)
         row_offs = np.zeros(na.size + 1, np.int64)
-        np.cumsum(na * nb, out=dist_offs[1:])
+        np.cumsum(na * ld, out=dist_offs[1:])
         np.cumsum(na, out=row_offs[1:])
         self.n_scenes, self.n_cams = int(n_scenes), int(n_cams)
         self.pairs = pairs
@@ -343,37 +358,51 @@ class PairwisePlan:
         self.max_rows = int(na.max()) if na.size else 0
         self.max_cols = int(nb.max()) if nb.size else 0
         self.max_n = max(self.max_rows, self.max_cols)
-        self.na, self.nb = na, nb
-        self.n_dist = int(dist_offs[-1])
+        self.na, self.nb, self.ld = na, nb, ld
+        self.row_align = row_align
+        self.n_dist = int((na * nb).sum())      # residuals (pairs)
+        self.dist_size = int(dist_offs[-1])     # floats of the (pitched) output
         self.n_rows = int(row_offs[-1])
         self.dist_offs_host, self.row_offs_host = dist_offs, row_offs
         self.device = torch.device(device)
         self.dist_offs, self.row_offs = _h2d_int64([dist_offs, row_offs], self.device)
 
     def matrix(self, dist: Tensor, scene: int, pair: int) -> Tensor:
-        """View of the (scene, pair) residual matrix inside a flat ``dist``."""
+        """(n_a, n_b) view of the (scene, pair) residual matrix inside ``dist``
+        (strided when the rows are pitched)."""
         sp = scene * len(self.pair_a) + pair
         o = int(self.dist_offs_host[sp])
-        na, nb = int(self.na[sp]), int(self.nb[sp])
-        return dist[o:o + na * nb].view(na, nb)
+        na, nb, ld = int(self.na[sp]), int(self.nb[sp]), int(self.ld[sp])
+        return dist[o:o + na * ld].view(na, ld)[:, :nb]
+
+    def compact(self, dist: Tensor) -> Tensor:
+        """The residuals in the unpitched layout (matrices back to back, rows
+        of n_b): ``dist`` itself when the plan is unpitched, else a copy."""
+        if self.dist_size == self.n_dist:
+            return dist[:self.n_dist]
+        parts = [self.matrix(dist, sp // len(self.pair_a), sp % len(self.pair_a)).reshape(-1)
+                 for sp in range(self.na.size)]
+        return torch.cat(parts) if parts else dist[:0]
 
 
 def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: PairwisePlan, *,
                              want_dist: bool = True,
                              out: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
                              options: Optional[dict] = None):
-    """-> (dist f32 [plan.n_dist], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
-    ``options``: mvm_options fields, e.g. ``{"pairwise_argmin": "eager"}``."""
+    """-> (dist f32 [plan.dist_size], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
+    ``dist`` has the plan's (possibly pitched) layout: ``plan.matrix()`` /
+    ``plan.compact()`` read it.  ``options``: mvm_options fields, e.g.
+    ``{"pairwise_argmin": "eager"}``."""
     dev = pts.device
     if out is None:
-        dist = torch.empty(plan.n_dist if want_dist else 0, dtype=torch.float32, device=dev)
+        dist = torch.empty(plan.dist_size if want_dist else 0, dtype=torch.float32, device=dev)
         argmin = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
         minval = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
     else:
         dist, argmin, minval = out
     torch.ops.mvmatch.pairwise_residual_argmin_out(
         pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_n,
-        plan.dist_offs, plan.row_offs, dist, argmin, minval, _opts_list(options))
+        plan.dist_offs, plan.row_offs, dist, argmin, minval, _opts_list(options), plan.row_align)
     return dist, argmin, minval
 
 

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 2
+#define MVM_ABI_VERSION 3
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -76,7 +76,8 @@ enum {
     MVM_PAIRWISE_ARGMIN_DEFAULT = 0,     /* = LAZY_TRANSPOSED */
     MVM_PAIRWISE_ARGMIN_LAZY_TRANSPOSED, /* clean row groups: per-chunk minimum bits,
                                             one LDS transpose per row group */
-    MVM_PAIRWISE_ARGMIN_LAZY_ROWS,       /* ... with per-row DPP reductions */
+    MVM_PAIRWISE_ARGMIN_LAZY_ROWS,       /* since ABI 3 an alias of LAZY_TRANSPOSED (the
+                                            per-row DPP form was removed) */
     MVM_PAIRWISE_ARGMIN_EAGER            /* best value + index per pair */
 };
 enum {
@@ -145,6 +146,24 @@ int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_of
                                     const int64_t *row_offs_dev, float *dist_dev,
                                     int32_t *argmin_dev, float *minval_dev,
                                     const mvm_options *opts, mvm_stream_t stream);
+
+/*
+ * The same with pitched rows (ABI 3): row i of matrix (s, p) starts at
+ *   dist_dev[dist_offs_dev[s*P + p] + i*ld],  ld = roundup(n_b, row_align),
+ * so with row_align 32 (and matrix offsets that are multiples of 32) every
+ * row starts on a 128-byte line and every store of a ragged view writes whole
+ * lines.  Columns n_b .. ld-1 of a row are padding: +inf where the kernel
+ * writes them, otherwise unspecified.  row_align is a power of two in
+ * [1, 256]; 1 is the unpitched layout of mvm_pairwise_residual_argmin_ex.
+ * The caller sizes dist_dev and dist_offs_dev with the pitched sizes n_a*ld.
+ */
+int mvm_pairwise_residual_argmin_pitched(const double *pts_dev, const int64_t *cam_offs_dev,
+                                         const double *F_dev, const int32_t *pair_a,
+                                         const int32_t *pair_b, int32_t n_scenes, int32_t n_cams,
+                                         int32_t n_pairs, int32_t max_n, int32_t row_align,
+                                         const int64_t *dist_offs_dev, const int64_t *row_offs_dev,
+                                         float *dist_dev, int32_t *argmin_dev, float *minval_dev,
+                                         const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * Same residuals kept in float64 (no cast), written with a uniform layout:

@@ -15,14 +15,20 @@ def _bits(a):
 
 
 def run_pairwise(dev, pts, cam_offs, F, pairs, S, C, want_dist=True, options=None):
+    """-> (residuals in the unpitched flat layout, argmin, minval).  ``options``
+    may carry "_row_align" (the plan's row pitch; default "auto")."""
     from bpc_baseline_amd import ops
-    plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=dev)
+    options = dict(options or {})
+    row_align = options.pop("_row_align", "auto")
+    plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=dev, row_align=row_align)
     d, a, m = ops.pairwise_residual_argmin(
         torch.from_numpy(np.ascontiguousarray(pts, np.float64)).to(dev),
         torch.from_numpy(np.ascontiguousarray(cam_offs, np.int64)).to(dev),
         torch.from_numpy(np.ascontiguousarray(F, np.float64)).to(dev), plan, want_dist=want_dist,
-        options=options)
+        options=options or None)
     torch.cuda.synchronize()
+    if want_dist:
+        d = plan.compact(d)
     return d.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
 
 
@@ -48,15 +54,17 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C, options=None):
 
 
 # ----------------------------------------------------------- pairwise ----
-@pytest.fixture(params=["default", "lazy_rows", "eager", "rpw8_rg2", "rpw4"])
+@pytest.fixture(params=["default", "unpitched", "eager", "eager_unpitched", "rpw8_rg2", "rpw4"])
 def argmin_path(request):
     """mvm_options of a pairwise kernel path: the lazy argmin (clean row
-    groups: per-chunk minimum, column recovered per group) with its transposed
-    LDS reduction (the default) and with per-row DPP reductions, the eager
-    argmin, and other row-group shapes (8 rows per wave x 2 groups, 4 rows
-    per wave)."""
-    return {"default": {}, "lazy_rows": {"pairwise_argmin": "lazy_rows"},
+    groups: per-chunk minimum bits, column recovered per group through one
+    LDS transpose; the default), the eager argmin, other row-group shapes (8
+    rows per wave x 2 groups, 4 rows per wave) -- each with the plan's default
+    row pitch (128-byte lines for ragged views) and the first two also
+    unpitched (rows of n_b, the unaligned-row paths)."""
+    return {"default": {}, "unpitched": {"_row_align": 1},
             "eager": {"pairwise_argmin": "eager"},
+            "eager_unpitched": {"pairwise_argmin": "eager", "_row_align": 1},
             "rpw8_rg2": {"pairwise_rows_per_wave": 8, "pairwise_row_groups": 2},
             "rpw4": {"pairwise_rows_per_wave": 4}}[request.param]
 
@@ -82,7 +90,7 @@ def test_pairwise_golden_4cam(cuda, golden):
     pts = np.concatenate(views)
     d, a, _ = run_pairwise(cuda, pts, cam_offs, g["F"], pairs, 1, 4)
     from bpc_baseline_amd.ops import PairwisePlan
-    plan = PairwisePlan(cam_offs, 1, 4, pairs, device="cpu")
+    plan = PairwisePlan(cam_offs, 1, 4, pairs, device="cpu", row_align=1)
     for p, (ca, cb) in enumerate(pairs):
         ref = g[f"e{ca}{cb}"]
         got = plan.matrix(torch.from_numpy(d), 0, p).numpy()
@@ -132,12 +140,11 @@ def test_pairwise_edge_cases(cuda, argmin_path):
 
 @pytest.mark.parametrize("counts", [(1000, 996, 1016, 1012), (72, 100, 132, 1020), (260, 4, 1000, 36)])
 def test_pairwise_rows_off_line_boundaries(cuda, counts, argmin_path):
-    """Float32 rows that do not start on a 128-byte line (n_b % 32 != 0,
-    n_b % 4 == 0): row groups of one alignment class (stride 2, 4 or 8) and
-    chunks shifted to the line holding column 0, with masked lanes before
-    column 0 and past n_b; views of different sizes in one scene, so the
-    matrices' offsets are misaligned too, and row counts that leave the last
-    block's classes partly filled."""
+    """Views whose counts are not multiples of 32 (n_b % 4 == 0): unpitched,
+    rows start mid-line and the lazy path masks the lanes past n_b in the
+    last chunk; pitched (the default), rows start on lines and the padding is
+    written.  Views of different sizes in one scene (misaligned matrix
+    offsets when unpitched), a degenerate pair and a NaN centroid."""
     rng = np.random.default_rng(sum(counts))
     S, C = 2, len(counts)
     cnt = np.array([counts, counts[::-1]], np.int64)
@@ -182,7 +189,7 @@ def test_pairwise_ties_and_duplicates(cuda, argmin_path):
     assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3, options=argmin_path)
 
 
-@pytest.mark.parametrize("n", [256, 512, 1024])
+@pytest.mark.parametrize("n", [256, 512, 1024, 600, 1000])
 def test_pairwise_row_minimum_ties(cuda, n, argmin_path):
     """Exact ties AT the row minimum in clean views (the lazy path's case):
     a row's winning column is duplicated inside its own 4-column lane group
@@ -200,6 +207,46 @@ def test_pairwise_row_minimum_ties(cuda, n, argmin_path):
         for j in {j0 ^ 1, j0 ^ 3, (j0 + 256) % n, (j0 + 4 * 7 + 1) % n, (j0 + 300) % n}:
             pts[ob + j] = pts[ob + j0]
     assert_pairwise_equal(cuda, pts, b.cam_offs, b.F, b.pairs, 2, 3, options=argmin_path)
+
+
+@pytest.mark.parametrize("row_align", [4, 32, 256])
+def test_pairwise_pitched_layout(cuda, row_align):
+    """mvm_pairwise_residual_argmin_pitched: row i of matrix (s, p) at
+    dist_offs[sp] + i * roundup(n_b, row_align).  Ragged IPD-like counts
+    (700..1024 and a few small views): every residual and argmin equal to the
+    oracle, every padding column +inf (clean views: the kernel writes whole
+    pitched rows), and nothing written past a matrix's pitched extent."""
+    from bpc_baseline_amd import ops
+    rng = np.random.default_rng(row_align)
+    S, C = 5, 4
+    cnt = rng.integers(700, 1025, size=(S, C))
+    cnt[1, 2], cnt[3, 0], cnt[4, 1] = 33, 1, 255
+    cam_offs = np.zeros(S * C + 1, np.int64)
+    np.cumsum(cnt.reshape(-1), out=cam_offs[1:])
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(S, C, 1024, seed=row_align)
+    pts = np.concatenate([b.pts[int(b.cam_offs[v]):int(b.cam_offs[v]) + int(cnt.reshape(-1)[v])]
+                          for v in range(S * C)])
+    plan = ops.PairwisePlan(cam_offs, S, C, b.pairs, device=cuda, row_align=row_align)
+    assert plan.row_align == row_align and np.all(plan.ld % row_align == 0)
+    assert np.all(plan.dist_offs_host % row_align == 0)
+    guard = plan.dist_size + 64
+    dist = torch.full((guard,), -7.0, dtype=torch.float32, device=cuda)
+    am = torch.empty(plan.n_rows, dtype=torch.int32, device=cuda)
+    mv = torch.empty(plan.n_rows, dtype=torch.float32, device=cuda)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    ops.pairwise_residual_argmin(t(pts), t(cam_offs), t(b.F), plan, out=(dist, am, mv))
+    torch.cuda.synchronize()
+    rd, ra, rm, _, _ = O.pairwise(pts, cam_offs, b.F, b.pairs, S, C)
+    assert np.array_equal(_bits(plan.compact(dist).cpu().numpy()), _bits(rd))
+    assert np.array_equal(am.cpu().numpy(), ra) and np.array_equal(_bits(mv.cpu().numpy()), _bits(rm))
+    h = dist.cpu().numpy()
+    for sp in range(plan.na.size):
+        o, na, nb, ld = (int(x) for x in (plan.dist_offs_host[sp], plan.na[sp], plan.nb[sp],
+                                           plan.ld[sp]))
+        pad = h[o:o + na * ld].reshape(na, ld)[:, nb:]
+        assert np.all(np.isposinf(pad)), f"matrix {sp}: padding not +inf"
+    assert np.all(h[plan.dist_size:] == -7.0)
 
 
 def test_pairwise_argmin_only(cuda, argmin_path):
@@ -294,7 +341,7 @@ def test_launches_capture_into_a_hip_graph(cuda):
     t = lambda a: torch.from_numpy(a).to(cuda)
     bp, bc, bF = t(b.pts), t(b.cam_offs), t(b.F)
     cp, cc, cF = t(c.pts), t(c.cam_offs), t(c.F)
-    dist = torch.empty(pp.n_dist, dtype=torch.float32, device=cuda)
+    dist = torch.empty(pp.dist_size, dtype=torch.float32, device=cuda)
     am = torch.empty(pp.n_rows, dtype=torch.int32, device=cuda)
     mv = torch.empty(pp.n_rows, dtype=torch.float32, device=cuda)
     cube = torch.empty(tp.n_cube, dtype=torch.float32, device=cuda)

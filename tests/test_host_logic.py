@@ -15,11 +15,45 @@ def test_pairwise_plan_offsets_match_oracle():
     from bpc_baseline_amd import ops
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(7, 4, 33, seed=2, ragged=True)
-    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu")
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu", row_align=1)
     doff, roff = O.pairwise_offsets(b.cam_offs, b.n_scenes, b.n_cams, b.pairs)
     assert np.array_equal(plan.dist_offs_host, doff) and np.array_equal(plan.row_offs_host, roff)
-    assert plan.n_dist == b.n_residual_pairs()
+    assert plan.n_dist == plan.dist_size == b.n_residual_pairs()
     assert plan.max_n == int(b.counts().max())
+
+
+@pytest.mark.parametrize("row_align", ["auto", 4, 32, 256])
+def test_pairwise_plan_pitched_rows(row_align):
+    """Pitched plans: ld = roundup(n_b, row_align); matrices back to back with
+    n_a * ld floats each; "auto" pitches to 32 floats (128-byte lines) when a
+    count is not a multiple of 32 and is unpitched otherwise; matrix() and
+    compact() read the unpitched values back."""
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    b = make_scenes(3, 4, 33, seed=2, ragged=True)
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu",
+                            row_align=row_align)
+    ra = 32 if row_align == "auto" else row_align
+    assert plan.row_align == ra
+    assert np.array_equal(plan.ld, (plan.nb + ra - 1) // ra * ra)
+    assert np.array_equal(np.diff(plan.dist_offs_host), plan.na * plan.ld)
+    assert plan.n_dist == b.n_residual_pairs() and plan.dist_size == int(plan.dist_offs_host[-1])
+    flat = O.pairwise(b.pts, b.cam_offs, b.F, b.pairs, b.n_scenes, b.n_cams)[0]
+    # lay the oracle's values out pitched (padding = +inf), read them back
+    pitched = np.full(plan.dist_size, np.inf, np.float32)
+    o = 0
+    for sp in range(plan.na.size):
+        na, nb, ld, d0 = (int(x) for x in (plan.na[sp], plan.nb[sp], plan.ld[sp],
+                                           plan.dist_offs_host[sp]))
+        pitched[d0:d0 + na * ld].reshape(na, ld)[:, :nb] = flat[o:o + na * nb].reshape(na, nb)
+        got = plan.matrix(torch.from_numpy(pitched), sp // 6, sp % 6).numpy()
+        assert np.array_equal(got, flat[o:o + na * nb].reshape(na, nb))
+        o += na * nb
+    assert np.array_equal(plan.compact(torch.from_numpy(pitched)).numpy(), flat)
+    u = ops.PairwisePlan(np.array([0, 64, 96], np.int64), 1, 2, [[0, 1]], device="cpu")
+    assert u.row_align == 1 and u.dist_size == u.n_dist == 64 * 32
+    with pytest.raises(ValueError):
+        ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu", row_align=48)
 
 
 def test_triplet_plan_offsets():

@@ -77,7 +77,7 @@ def add_contiguous():
 if args.contiguous and args.first == "contiguous":
     add_contiguous()
 for i in range(args.buffers):
-    bufs[f"torch{i}"] = torch.empty(plan.n_dist, dtype=torch.float32, device=dev)
+    bufs[f"torch{i}"] = torch.empty(plan.dist_size if hasattr(plan, "dist_size") else plan.n_dist, dtype=torch.float32, device=dev)
 if args.contiguous and args.first == "torch":
     add_contiguous()
 for name, t in bufs.items():

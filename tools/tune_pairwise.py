@@ -51,7 +51,7 @@ plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
 pts = torch.from_numpy(b.pts).to(dev)
 co = torch.from_numpy(b.cam_offs).to(dev)
 F = torch.from_numpy(b.F).to(dev)
-dist = torch.empty(0 if args.no_dist else plan.n_dist, dtype=torch.float32, device=dev)
+dist = torch.empty(0 if args.no_dist else plan.dist_size, dtype=torch.float32, device=dev)
 am = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.int32, device=dev)
 mv = torch.empty(0 if args.no_argmin else plan.n_rows, dtype=torch.float32, device=dev)
 nbytes = (16.0 * b.pts.shape[0] + 72.0 * b.F.shape[0] + (0 if args.no_dist else 4.0 * plan.n_dist)
