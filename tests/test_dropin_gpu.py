@@ -336,3 +336,35 @@ def test_cached_slots_across_shapes_and_repeats(cuda):
             want = [(r // M, r % M, k) for r, k in zip(r0, c0) if flat[r, k] < 30]
             got = [tuple(int(x) for x in m) for m in match_objects(c, 30)]
             assert got == [tuple(int(x) for x in m) for m in want], (it, c.dtype)
+
+
+def test_capacity_slots_cover_changing_counts(cuda):
+    """Real captures change their detection counts from one call to the next:
+    counts cycling over 1..8 per view (> 32 distinct shapes) all run through
+    ONE capacity-class cube slot and one assignment slot per dtype, and every
+    call equals the oracle cube and scipy's matches."""
+    from scipy.optimize import linear_sum_assignment as scipy_lsa
+    from bpc_baseline_amd.inference import capture_session as cs
+    from bpc_baseline_amd.inference.epipolar_matching import compute_cost_matrix, match_objects
+    from bpc_baseline_amd.synth import make_scenes
+    cs.clear()
+    rng = np.random.default_rng(8)
+    shapes = {tuple(int(x) for x in rng.integers(1, 9, 3)) for _ in range(200)}
+    assert len(shapes) > 32
+    for it, counts in enumerate(sorted(shapes)):
+        b = make_scenes(1, 3, list(counts), seed=900 + it)
+        views = [b.pts[b.cam_offs[c]:b.cam_offs[c + 1]] for c in range(3)]
+        F = b.F.reshape(3, 3, 3)
+        cube = compute_cost_matrix(_dets(views[0]), _dets(views[1]), _dets(views[2]), F[0], F[1], F[2])
+        ref = O.cube(b.pts, b.cam_offs, b.F, 1)[0].reshape(counts)
+        assert np.array_equal(_b32(cube), _b32(ref)), counts
+        N, M, P = cube.shape
+        flat = cube.reshape(N * M, P)
+        r0, c0 = scipy_lsa(flat)
+        want = [(r // M, r % M, k) for r, k in zip(r0, c0) if flat[r, k] < 30]
+        assert [tuple(int(x) for x in m) for m in match_objects(cube, 30)] == \
+            [tuple(int(x) for x in m) for m in want], counts
+    info = cs.cache_info()
+    assert info["cube"]["slots"] == 1            # every view <= 8: capacity class 8
+    assert info["lsap"]["slots"] <= 4            # rows <= 64 (classes 8..64) x cols <= 8
+    cs.clear()

@@ -441,3 +441,32 @@ def test_bench_rejects_fewer_scenes_than_ranks(monkeypatch):
     with pytest.raises(SystemExit, match="every rank needs at least one scene"):
         bench.main()
     assert distributed.shard_range(4, 7, 8) == (4, 4)
+
+
+def test_capture_session_cache_bounds(monkeypatch):
+    """The drop-in's slot cache: capacity classes (next power of two, >= 8),
+    LRU eviction by count AND bytes, a slot above the byte cap used uncached,
+    and clear() releasing the thread's slots (no unbounded pinned /
+    device memory in a long-lived service)."""
+    from bpc_baseline_amd.inference import capture_session as cs
+    assert [cs._cap(n) for n in (0, 1, 8, 9, 24, 64, 65)] == [8, 8, 8, 16, 32, 64, 128]
+
+    class Fake:
+        def __init__(self, nbytes):
+            self.nbytes = nbytes
+
+    cs.clear()
+    monkeypatch.setattr(cs, "_MAX_BYTES", 1000)
+    monkeypatch.setattr(cs, "_MAX_SLOTS", 3)
+    for k in range(5):                                   # count bound
+        cs._lookup("cube", ("c", k), lambda: Fake(10))
+    assert cs.cache_info()["cube"] == {"slots": 3, "bytes": 30}
+    assert ("c", 4) in cs._cache("cube") and ("c", 0) not in cs._cache("cube")
+    a = cs._lookup("cube", ("c", 2), lambda: Fake(10))  # a hit moves to the end
+    assert list(cs._cache("cube"))[-1] == ("c", 2) and a is cs._cache("cube")[("c", 2)]
+    cs._lookup("cube", ("big", 0), lambda: Fake(980))   # byte bound evicts the oldest
+    assert cs.cache_info()["cube"]["bytes"] <= 1000
+    huge = cs._lookup("cube", ("huge", 0), lambda: Fake(5000))
+    assert huge.nbytes == 5000 and ("huge", 0) not in cs._cache("cube")
+    cs.clear()
+    assert cs.cache_info() == {"cube": {"slots": 0, "bytes": 0}, "lsap": {"slots": 0, "bytes": 0}}

@@ -144,7 +144,57 @@ def main():
                      "reps": {"gpu": k_gpu, "cpu": k_cpu}})
         print(f"n={n}: gpu {t_gpu:.3f} ms (cube {t_gcube:.3f}, lsap {t_glsap:.3f}, _match {t_gmatch:.3f}) "
               f"cpu {t_cpu:.3f} ms (_match {t_cmatch:.3f})", file=sys.stderr)
+    # mixed shapes: consecutive calls with different detection counts (1..8
+    # per view, > 32 distinct shapes, as a real capture stream has): every
+    # call a different (N, M, P), so no call repeats the previous one's shape
+    rng = np.random.default_rng(7)
+    shapes = sorted({tuple(int(x) for x in rng.integers(1, 9, 3)) for _ in range(400)})
+    rng.shuffle(shapes)
+    calls = []
+    for q, counts in enumerate(shapes):
+        Ks, RTs, dets = make_capture(np.random.default_rng(5000 + q), 3, max(counts))
+        dd = [dets[c][:counts[c]] for c in range(3)]
+        R = [rt[:3, :3] for rt in RTs]
+        t = [rt[:3, 3] for rt in RTs]
+        Fs = (compute_fundamental_matrix(Ks[0], R[0], t[0], Ks[1], R[1], t[1]),
+              compute_fundamental_matrix(Ks[0], R[0], t[0], Ks[2], R[2], t[2]),
+              compute_fundamental_matrix(Ks[1], R[1], t[1], Ks[2], R[2], t[2]))
+        calls.append((dd, Fs))
+    from bpc_baseline_amd.inference import capture_session
+    capture_session.clear()
+
+    def sweep(gpu):
+        ts, res = [], []
+        for dd, Fs in calls:
+            t0 = time.perf_counter()
+            if gpu:
+                cube = em.compute_cost_matrix(*dd, *Fs)
+                m = [tuple(int(v) for v in q) for q in em.match_objects(cube, args.threshold)]
+            else:
+                cube = RL.cube(*([d["bb_center"] for d in v] for v in dd), *Fs)
+                m = cpu_match_objects(cube, args.threshold)
+            ts.append(time.perf_counter() - t0)
+            res.append(m)
+        return ts, res
+
+    g_cold, g_res = sweep(True)       # first pass: includes every slot build (cold)
+    g_warm, _ = sweep(True)
+    c_ts, c_res = sweep(False)
+    assert g_res == c_res
+    mixed = {"distinct_shapes": len(calls), "counts": "1..8 per view, shuffled",
+             "gpu_ms_median_first_pass": statistics.median(g_cold) * 1e3,
+             "gpu_ms_first_call": g_cold[0] * 1e3,
+             "gpu_ms_median_second_pass": statistics.median(g_warm) * 1e3,
+             "cpu_ms_median": statistics.median(c_ts) * 1e3,
+             "slots_after": capture_session.cache_info(),
+             "note": "cost_matrix+match_objects per call; the first pass includes building the "
+                     "capacity-class slots (one cube slot and a few assignment slots for all "
+                     "shapes), first_call the very first build"}
+    print(f"mixed: gpu {mixed['gpu_ms_median_first_pass']:.3f} ms first pass, "
+          f"{mixed['gpu_ms_median_second_pass']:.3f} ms second; cpu {mixed['cpu_ms_median']:.3f} ms",
+          file=sys.stderr)
     out = {"what": "drop-in matching stage latency per capture (wall clock, median)",
+           "mixed_shapes": mixed,
            "cpu": platform.processor() or platform.machine(), "cpu_cores": 1,
            "gpu": torch.cuda.get_device_name(0), "rows": rows}
     print(json.dumps(out))
