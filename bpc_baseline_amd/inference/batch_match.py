@@ -31,44 +31,10 @@ import numpy as np
 import torch
 
 from .. import ops
-from .utils.camera_utils import camera_pairs, fundamental_matrices_batched
+from .utils.camera_utils import projection_matrices, rig_matrices
 
 __all__ = ["MatchBatch", "match_capture_stream", "match_captures", "projection_matrices",
-           "rig_matrices"]
-
-
-def projection_matrices(Ks: np.ndarray, RTs: np.ndarray) -> np.ndarray:
-    """P = K @ RT[:3] per camera (process_pose.py:91: float32 K promoted to
-    float64 by the product with the float64 RT) -> float64 [S, C, 3, 4]."""
-    return np.ascontiguousarray(np.asarray(Ks) @ np.asarray(RTs, dtype=np.float64)[..., :3, :])
-
-
-def rig_matrices(Ks: np.ndarray, RTs: np.ndarray):
-    """F (f64 [S*3, 9]) and P (f64 [S, 3, 3, 4]) of every capture, computed once
-    per DISTINCT rig: captures whose K and RT bytes are identical (a static
-    camera rig, as within an IPD scene) share one evaluation, so the values
-    are bit-identical to evaluating each capture."""
-    S = Ks.shape[0]
-    kb = np.ascontiguousarray(Ks).reshape(S, -1).view(np.uint32)
-    rb = np.ascontiguousarray(RTs).reshape(S, -1).view(np.uint64)
-    if S > 1 and (kb == kb[0]).all() and (rb == rb[0]).all():
-        first, inv = np.zeros(1, np.int64), np.zeros(S, np.int64)
-    elif S > 1 and len(np.unique(rb[:, 3])) == S:   # camera 0's t_x already tells them apart
-        first, inv = None, None
-    elif S > 1:
-        key = np.ascontiguousarray(np.concatenate([kb.view(np.uint8), rb.view(np.uint8)], axis=1))
-        kv = key.view(np.dtype((np.void, key.shape[1]))).reshape(-1)
-        _, first, inv = np.unique(kv, return_index=True, return_inverse=True)
-        inv = inv.reshape(-1)
-        if len(first) == S:
-            first, inv = None, None
-    else:
-        first, inv = None, None
-    if first is None:
-        return fundamental_matrices_batched(Ks, RTs, camera_pairs(3)), projection_matrices(Ks, RTs)
-    Fu = fundamental_matrices_batched(Ks[first], RTs[first], camera_pairs(3)).reshape(len(first), 3, 9)
-    Pu = projection_matrices(Ks[first], RTs[first])
-    return np.ascontiguousarray(Fu[inv].reshape(S * 3, 9)), np.ascontiguousarray(Pu[inv])
+           "rig_matrices", "rig_worker_pool"]
 
 
 @dataclass
@@ -187,37 +153,56 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                       cube=cube if keep_cube else None)
 
 
-def _rig_host(batch: Sequence):
-    """F and P of one ``match_capture_stream`` batch on the host (numpy)."""
+def _rig_inputs(batch: Sequence):
+    """(Ks f32 [S,3,3,3], RTs f64 [S,3,4,4]) of one ``match_capture_stream`` batch."""
     boxes, conf, cls, img_offs, Ks, RTs = batch
     S = (int(img_offs.numel()) - 1) // 3
-    return rig_matrices(np.asarray(Ks, dtype=np.float32).reshape(S, 3, 3, 3),
-                        np.asarray(RTs, dtype=np.float64).reshape(S, 3, 4, 4))
+    return (np.asarray(Ks, dtype=np.float32).reshape(S, 3, 3, 3),
+            np.asarray(RTs, dtype=np.float64).reshape(S, 3, 4, 4))
 
 
-def match_capture_stream(batches: Iterable[Sequence], **kwargs) -> Iterator[MatchBatch]:
+_POOL = {}
+
+
+def rig_worker_pool(n: int):
+    """The process-wide ``RigWorkers`` of ``n`` processes (started on first use,
+    reused by every stream, closed at exit)."""
+    from .rig_workers import RigWorkers
+    pool = _POOL.get(n)
+    if pool is None:
+        import atexit
+        pool = _POOL[n] = RigWorkers(n)
+        atexit.register(pool.close)
+    return pool
+
+
+def match_capture_stream(batches: Iterable[Sequence], *, rig_workers: int = 3,
+                         **kwargs) -> Iterator[MatchBatch]:
     """``match_captures`` over a sequence of batches, pipelined: the host F and
-    P of batch b+1 (``rig_matrices``, numpy) are computed on a worker thread
-    while batch b's device chain runs and the main thread waits on its two
-    device->host copies.  Each batch is ``(boxes, conf, cls, img_offs, Ks,
-    RTs)`` as ``match_captures`` takes them; ``kwargs`` are passed through
-    (``F`` / ``proj`` are computed here).  Results equal ``match_captures`` on
-    each batch: the same F and P arithmetic, only earlier.
+    P of batch b+1 (``rig_matrices``: numpy, the same function, so the same
+    bits) are computed by ``rig_workers`` worker PROCESSES
+    (``rig_workers.RigWorkers``, shared memory) while the main process runs
+    batch b's device chain -- off its GIL, which a worker thread was not
+    (DESIGN.md §3.10).  ``rig_workers=0`` computes them inline.  Each batch is
+    ``(boxes, conf, cls, img_offs, Ks, RTs)`` as ``match_captures`` takes them;
+    ``kwargs`` are passed through (``F`` / ``proj`` are computed here).
+    Results equal ``match_captures`` on each batch.
     """
-    from concurrent.futures import ThreadPoolExecutor
     if "F" in kwargs or "proj" in kwargs:
         raise TypeError("match_capture_stream computes F and proj itself")
     it = iter(batches)
     cur = next(it, None)
     if cur is None:
         return
-    with ThreadPoolExecutor(max_workers=1) as pool:
-        fut = pool.submit(_rig_host, cur)
-        while cur is not None:
-            nxt = next(it, None)
-            fut_next = pool.submit(_rig_host, nxt) if nxt is not None else None
-            F_h, P_h = fut.result()
-            dev = cur[0].device
-            yield match_captures(*cur, F=torch.from_numpy(F_h).to(dev),
-                                 proj=torch.from_numpy(P_h).to(dev), **kwargs)
-            cur, fut = nxt, fut_next
+    pool = rig_worker_pool(rig_workers) if rig_workers > 0 else None
+    if pool is not None:
+        pool.submit(*_rig_inputs(cur))
+    while cur is not None:
+        F_h, P_h = pool.result() if pool is not None else rig_matrices(*_rig_inputs(cur))
+        nxt = next(it, None)
+        if nxt is not None and pool is not None:
+            pool.submit(*_rig_inputs(nxt))       # batch b+1's F/P while batch b runs
+        dev = cur[0].device
+        yield match_captures(*cur, F=torch.from_numpy(F_h).to(dev),
+                             proj=torch.from_numpy(P_h).to(dev), **kwargs)
+        cur = nxt

@@ -25,6 +25,9 @@ __all__ = [
     "calc_pose_matrix",
     "camera_pairs",
     "fundamental_matrices",
+    "fundamental_matrices_batched",
+    "projection_matrices",
+    "rig_matrices",
 ]
 
 
@@ -162,3 +165,37 @@ def fundamental_matrices_batched(Ks: np.ndarray, RTs: np.ndarray, pairs: np.ndar
     f22 = F[..., 2:3, 2:3]
     F = np.where(np.abs(f22) > 1e-8, F / np.where(np.abs(f22) > 1e-8, f22, 1.0), F)
     return np.ascontiguousarray(F.reshape(-1, 9), dtype=np.float64)
+
+
+def projection_matrices(Ks: np.ndarray, RTs: np.ndarray) -> np.ndarray:
+    """P = K @ RT[:3] per camera (process_pose.py:91: float32 K promoted to
+    float64 by the product with the float64 RT) -> float64 [S, C, 3, 4]."""
+    return np.ascontiguousarray(np.asarray(Ks) @ np.asarray(RTs, dtype=np.float64)[..., :3, :])
+
+
+def rig_matrices(Ks: np.ndarray, RTs: np.ndarray):
+    """F (f64 [S*3, 9]) and P (f64 [S, 3, 3, 4]) of every capture, computed once
+    per DISTINCT rig: captures whose K and RT bytes are identical (a static
+    camera rig, as within an IPD scene) share one evaluation, so the values
+    are bit-identical to evaluating each capture."""
+    S = Ks.shape[0]
+    kb = np.ascontiguousarray(Ks).reshape(S, -1).view(np.uint32)
+    rb = np.ascontiguousarray(RTs).reshape(S, -1).view(np.uint64)
+    if S > 1 and (kb == kb[0]).all() and (rb == rb[0]).all():
+        first, inv = np.zeros(1, np.int64), np.zeros(S, np.int64)
+    elif S > 1 and len(np.unique(rb[:, 3])) == S:   # camera 0's t_x already tells them apart
+        first, inv = None, None
+    elif S > 1:
+        key = np.ascontiguousarray(np.concatenate([kb.view(np.uint8), rb.view(np.uint8)], axis=1))
+        kv = key.view(np.dtype((np.void, key.shape[1]))).reshape(-1)
+        _, first, inv = np.unique(kv, return_index=True, return_inverse=True)
+        inv = inv.reshape(-1)
+        if len(first) == S:
+            first, inv = None, None
+    else:
+        first, inv = None, None
+    if first is None:
+        return fundamental_matrices_batched(Ks, RTs, camera_pairs(3)), projection_matrices(Ks, RTs)
+    Fu = fundamental_matrices_batched(Ks[first], RTs[first], camera_pairs(3)).reshape(len(first), 3, 9)
+    Pu = projection_matrices(Ks[first], RTs[first])
+    return np.ascontiguousarray(Fu[inv].reshape(S * 3, 9)), np.ascontiguousarray(Pu[inv])

@@ -470,3 +470,36 @@ def test_capture_session_cache_bounds(monkeypatch):
     assert huge.nbytes == 5000 and ("huge", 0) not in cs._cache("cube")
     cs.clear()
     assert cs.cache_info() == {"cube": {"slots": 0, "bytes": 0}, "lsap": {"slots": 0, "bytes": 0}}
+
+
+def test_rig_workers_equal_rig_matrices():
+    """F and P computed by the worker processes (shared memory, slices of the
+    batch per worker) equal rig_matrices in the calling process bit for bit:
+    a static rig, mixed rigs, all distinct, a batch larger than the slots
+    (the slot grows), an empty batch, and submit-before-collect pipelining."""
+    from bpc_baseline_amd.synth import make_rig
+    from bpc_baseline_amd.inference.rig_workers import RigWorkers
+    from bpc_baseline_amd.inference.utils.camera_utils import rig_matrices
+    rng = np.random.default_rng(12)
+
+    def batch(S, n_rigs):
+        rigs = [make_rig(rng, 3) for _ in range(n_rigs)]
+        idx = rng.integers(0, n_rigs, S)
+        Ks = np.stack([np.stack(rigs[i][0]) for i in idx]).astype(np.float32)
+        RTs = np.stack([np.stack(rigs[i][1]) for i in idx]).astype(np.float64)
+        return Ks, RTs
+
+    empty = (np.zeros((0, 3, 3, 3), np.float32), np.zeros((0, 3, 4, 4), np.float64))
+    batches = [batch(40, 1), batch(64, 5), batch(300, 300), batch(7, 7), empty]
+    with RigWorkers(3) as rw:
+        rw.submit(*batches[0])
+        for k, (Ks, RTs) in enumerate(batches):
+            F, P = rw.result()
+            if k + 1 < len(batches):
+                rw.submit(*batches[k + 1])
+            if Ks.shape[0] == 0:
+                assert F.shape == (0, 9) and P.shape == (0, 3, 3, 4)
+                continue
+            Fr, Pr = rig_matrices(Ks, RTs)
+            assert np.array_equal(F.view(np.int64), Fr.view(np.int64)), k
+            assert np.array_equal(P.view(np.int64), Pr.view(np.int64)), k
