@@ -56,7 +56,20 @@ struct LsapArgs {
     unsigned char *sync;        // per-problem barrier + reduction slots (multi kernel)
     int32_t lds_max_cols;       // long sides in (wave_max_cols, this]: column state in LDS
     int32_t lds_small_cols;     // ... of which those up to this: 256-thread LDS kernel
+    int32_t reg_max_cols;       // long sides in (wave_max_cols, this] with short sides <=
+                                // kRegMaxShort: lsap_reg_kernel (column state in VGPRs)
+    int32_t reg_nc_cap, reg_nr_cap;   // its dynamic LDS sizing (columns, rows)
 };
+
+// lsap_reg_kernel's class: short sides up to this (its row state is in LDS)
+constexpr int kRegMaxShort = 1024;
+constexpr int kRegMaxCols = 4096;      // 512 threads x 8 columns, or 1024 x 4
+
+__device__ __forceinline__ bool in_reg_class(const LsapArgs &a, int64_t R, int64_t K) {
+    const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
+    return a.reg_max_cols > 0 && lng > a.wave_max_cols && lng <= a.reg_max_cols &&
+           sht <= kRegMaxShort;
+}
 
 // Column state of lsap_kernel<.., true> in LDS: spc, v (f64), path, row4col,
 // pos, rem (i32) = 32 bytes per long-side column.
@@ -169,6 +182,7 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     }
     if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
     if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
+    if (in_reg_class(a, R, K)) return;                 // solved by lsap_reg_kernel
     const int64_t longside = R > K ? R : K;
     // class of the problem: LDS state with 256 threads (long side <= lds_small)
     // or 1024 threads, then workspace state with 256 or 1024 threads
@@ -594,6 +608,64 @@ __global__ __launch_bounds__(64 * kWaveProblems) void lsap_wave_kernel(LsapArgs 
 }
 
 
+// -------------------------- one workgroup per problem, state in VGPRs ----
+// Long sides of 1,025 .. 4,096 columns (the flattened cubes of 33-64
+// detections per view: 4096 x 64) with short sides <= kRegMaxShort.  The
+// wave kernel's layout over a whole workgroup: thread t keeps the state of
+// columns t, t + NT, ... (K of them: spc, v, path, row4col, scan position)
+// in registers, so a Dijkstra step reads no column state from memory, only
+// the current cost row (coalesced).  Per step every wave reduces its
+// candidates with the tie rule (mred_wave: the winner's column and row4col
+// travel with it), publishes one record, and after ONE barrier every wave
+// combines the NT/64 records in the same order -- no serial thread-0 stage,
+// no second barrier (the records alternate between two buffers).  The swap-
+// with-last removal is done by the owners of the chosen column and of the
+// column at the last scan position.  Row duals and col4row live in LDS;
+// augmentation walks the path through an LDS copy of the visited columns'
+// path entries, marking each path column with its new row, which the owners
+// read back.  Against the LDS-state kernel it needs ~20 B of LDS per column
+// instead of 32 B of state read and written every step, and no rem array.
+template <typename CT, int NT>
+__device__ __forceinline__ bool validate_transpose(const LsapArgs &a, const CT *C0, CT *Ctw,
+                                                   int64_t R, int64_t K, int64_t nc, bool transpose,
+                                                   CT (*s_tile)[kTile * 4 / sizeof(CT) + 1],
+                                                   int *s_flag) {
+    constexpr int kT = kTile * 4 / (int)sizeof(CT);
+    const int t = threadIdx.x;
+    if (t == 0) *s_flag = 0;
+    __syncthreads();
+    int bad = 0;
+    if (transpose) {
+        for (int64_t r0 = 0; r0 < R; r0 += kT) {
+            for (int64_t c0 = 0; c0 < K; c0 += kT) {
+                for (int x = t; x < kT * kT; x += NT) {
+                    const int rr = x / kT, cc = x % kT;
+                    CT val = 0;
+                    if (r0 + rr < R && c0 + cc < K) {
+                        val = C0[(r0 + rr) * K + c0 + cc];
+                        bad |= (val != val) || (val == -INFINITY);
+                    }
+                    s_tile[rr][cc] = val;
+                }
+                __syncthreads();
+                for (int x = t; x < kT * kT; x += NT) {
+                    const int cc = x / kT, rr = x % kT;
+                    if (r0 + rr < R && c0 + cc < K) Ctw[(c0 + cc) * nc + r0 + rr] = s_tile[rr][cc];
+                }
+                __syncthreads();
+            }
+        }
+    } else {
+        for (int64_t x = t; x < R * K; x += NT) {
+            const CT val = C0[x];
+            bad |= (val != val) || (val == -INFINITY);
+        }
+    }
+    if (bad) atomicOr(s_flag, 1);
+    __syncthreads();
+    return *s_flag == 0;
+}
+
 // --------------------------------------- G workgroups per problem ----
 // For few large problems (a single 256^3 scene: 65,536 columns) one CU
 // streaming all the column state per Dijkstra step is the bottleneck.  Here G
@@ -691,6 +763,180 @@ __device__ bool group_barrier(SyncBlock *sb, unsigned int target) {
     }
     __syncthreads();
     return s_ok;
+}
+
+// OCC: waves per SIMD to fit (512 threads: 4 -> two workgroups per CU at <= 128 VGPRs)
+template <typename CT, int NT, int K, int OCC = (NT == 512 ? 4 : 1)>
+__global__ __launch_bounds__(NT, OCC) void lsap_reg_kernel(LsapArgs a) {
+    constexpr int kNW = NT / 64;
+    constexpr int kT = kTile * 4 / (int)sizeof(CT);
+    __shared__ CT s_tile[kT][kT + 1];
+    __shared__ Red s_rec[2][kNW];
+    __shared__ int s_flag;
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    static_assert(NT * K <= 4096, "scan keys hold 12-bit positions and columns");
+
+    const int t = threadIdx.x, lane = t % 64, wave = t / 64;
+    const int p = blockIdx.x;
+    const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+    if (R == 0 || Kd == 0) {
+        if (t == 0) a.status[p] = 0;
+        return;
+    }
+    if (a.multi_g > 1 || !in_reg_class(a, R, Kd)) return;   // another kernel's problem
+    const bool transpose = Kd < R;
+    const int nr = (int)(transpose ? Kd : R), nc = (int)(transpose ? R : Kd);
+    const Layout L = lsap_layout(nr, nc, transpose, sizeof(CT));
+    unsigned char *w = a.ws + a.ws_offs[p];
+    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
+    const CT *Ct = transpose ? reinterpret_cast<const CT *>(w + L.ct) : C0;
+    // LDS: row duals and col4row [reg_nr_cap], per column path and row4col [reg_nc_cap]
+    double *u = reinterpret_cast<double *>(s_dyn);
+    int32_t *c4r = reinterpret_cast<int32_t *>(u + a.reg_nr_cap);
+    int32_t *s_path = c4r + a.reg_nr_cap;
+    int32_t *s_r4c = s_path + a.reg_nc_cap;
+
+    if (!validate_transpose<CT, NT>(a, C0, reinterpret_cast<CT *>(w + L.ct), R, Kd, nc, transpose,
+                                    s_tile, &s_flag)) {
+        if (t == 0) a.status[p] = 1;
+        return;
+    }
+    for (int i = t; i < nr; i += NT) {
+        u[i] = 0.0;
+        c4r[i] = -1;
+    }
+    for (int j = t; j < nc; j += NT) s_r4c[j] = -1;
+    // per column, in registers: spc, v, scan position; bit q of `freem`:
+    // column t + NT*q has no row yet (row4col == -1)
+    double spc[K], v[K];
+    int32_t pos[K];
+    uint32_t freem = (1u << K) - 1;
+#pragma unroll
+    for (int q = 0; q < K; ++q) v[q] = 0.0;
+    int par = 0;
+    for (int cur = 0; cur < nr; ++cur) {
+        uint32_t insc = 0;
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            const int j = t + NT * q;
+            spc[q] = INFINITY;
+            pos[q] = j < nc ? nc - 1 - j : -1;   // scan array starts in reverse column order
+        }
+        int i = cur, sink = -1, nrem = nc;
+        double min_val = 0.0;
+        __syncthreads();                          // u / c4r / s_r4c of the previous row are in place
+        while (sink < 0) {
+            const double ui = u[i];
+            const CT *Ci = Ct + (int64_t)i * nc;
+            CT cq[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) cq[q] = Ci[min(t + NT * q, nc - 1)];   // all loads first
+            // candidates keyed (scan position << 12 | column): positions are
+            // unique, so the smallest key is the first minimum in scan order
+            // and the largest free key the last free one -- the wave kernel's
+            // Red and its DPP reduction carry the columns along
+            Red best{INFINITY, 0x7FFFFFFF, -1};
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                if (pos[q] < 0) continue;         // visited, or past the columns
+                const int32_t j = t + NT * q;
+                const double r = ((min_val + (double)cq[q]) - ui) - v[q];
+                if (r < spc[q]) {
+                    s_path[j] = i;
+                    spc[q] = r;
+                }
+                const double sq = spc[q];
+                const int32_t key = (pos[q] << 12) | j;
+                const bool fr = (freem >> q) & 1u;
+                if (sq < best.m) {
+                    best.m = sq;
+                    best.first = key;
+                    best.last_free = fr ? key : -1;
+                } else if (sq == best.m) {
+                    best.first = min(best.first, key);
+                    if (fr) best.last_free = max(best.last_free, key);
+                }
+            }
+            best = red_wave_dpp(best);
+            if (lane == 0) s_rec[par][wave] = best;
+            __syncthreads();
+            // every wave combines the kNW records: lane k < kNW reads record k,
+            // DPP steps over those lanes (the combine is commutative and
+            // associative), so every wave holds the same result
+            Red r{INFINITY, 0x7FFFFFFF, -1};
+            if (lane < kNW) r = s_rec[par][lane];
+            r = red_dpp_step<0xB1>(r);
+            r = red_dpp_step<0x4E>(r);
+            if (kNW > 4) r = red_dpp_step<0x141>(r);
+            if (kNW > 8) r = red_dpp_step<0x140>(r);
+            r = red_readlane(r, 0);
+            par ^= 1;
+            if (!(r.m < INFINITY)) {              // uniform over the workgroup
+                if (t == 0) a.status[p] = 2;      // infeasible
+                return;
+            }
+            const int32_t key = r.last_free >= 0 ? r.last_free : r.first;
+            const int32_t index = key >> 12, j = key & 0xFFF;
+            const int32_t r4 = r.last_free >= 0 ? -1 : s_r4c[j];
+            --nrem;
+#pragma unroll
+            for (int q = 0; q < K; ++q) {         // swap-with-last removal, by the owners
+                if (pos[q] == nrem) pos[q] = index;   // the last scan position moves to index
+                if (t + NT * q == j) {                // (after: last == j leaves j removed)
+                    pos[q] = -1;
+                    insc |= 1u << q;
+                }
+            }
+            min_val = r.m;
+            if (r4 == -1) sink = j;
+            else i = r4;
+        }
+        // dual updates, column-driven: a visited row i != cur is row4col[j] of
+        // exactly one visited column j; cur itself has no column yet
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            if (insc & (1u << q)) {
+                const int32_t ri = s_r4c[t + NT * q];
+                if (ri != -1) u[ri] += min_val - spc[q];
+                v[q] -= min_val - spc[q];
+            }
+        }
+        if (t == 0) u[cur] += min_val;
+        __syncthreads();
+        if (t == 0) {                             // augment along the path
+            int j = sink;
+            while (true) {
+                const int i2 = s_path[j];
+                s_r4c[j] = i2;
+                const int prev = c4r[i2];
+                c4r[i2] = j;
+                j = prev;
+                if (i2 == cur) break;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < K; ++q)               // path columns (all visited) now have rows
+            if ((insc >> q) & 1u) freem &= s_r4c[t + NT * q] == -1 ? ~0u : ~(1u << q);
+    }
+    __syncthreads();
+    // output pairs in scipy's order
+    const int64_t o = a.out_offs[p];
+    if (transpose) {
+        for (int k = t; k < nr; k += NT) {
+            const int32_t rk = c4r[k];
+            int rank = 0;
+            for (int k2 = 0; k2 < nr; ++k2) rank += c4r[k2] < rk;
+            a.row_ind[o + rank] = rk;
+            a.col_ind[o + rank] = k;
+        }
+    } else {
+        for (int k = t; k < nr; k += NT) {
+            a.row_ind[o + k] = k;
+            a.col_ind[o + k] = c4r[k];
+        }
+    }
+    if (t == 0) a.status[p] = 0;
 }
 
 template <typename CT>
@@ -1014,6 +1260,30 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
             a.multi_g = 0;                     // fall back to one workgroup per problem
         }
     }
+    // long sides in (wave_max, lsap_reg_max_cols] with short sides <= 1024:
+    // one workgroup per problem with the column state in registers
+    int reg_max = o.lsap_reg_max_cols == 0 ? kRegMaxCols : o.lsap_reg_max_cols;
+    reg_max = reg_max < 0 ? 0 : (reg_max > kRegMaxCols ? kRegMaxCols : reg_max);
+    a.reg_max_cols = reg_max > wave_max ? reg_max : 0;
+    if (a.multi_g <= 1 && big && a.reg_max_cols > 0 && overlaps((int64_t)wave_max + 1, a.reg_max_cols)) {
+        a.reg_nc_cap = (int32_t)(long_max < a.reg_max_cols ? long_max : a.reg_max_cols);
+        a.reg_nr_cap = (int32_t)(long_max < kRegMaxShort ? long_max : kRegMaxShort);
+        const size_t lds = (size_t)a.reg_nc_cap * 8 + (size_t)a.reg_nr_cap * 12;
+        // 512 threads x 8 columns: ~100 VGPRs, two workgroups per CU
+        const bool wide = o.lsap_reg_threads == 1024;
+        if (o.lsap_reg_threads != 0 && o.lsap_reg_threads != 512 && !wide)
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "lsap_reg_threads %d not 512 or 1024",
+                            (int)o.lsap_reg_threads);
+        const void *kern = wide ? reinterpret_cast<const void *>(&lsap_reg_kernel<CT, 1024, 4>)
+                                : reinterpret_cast<const void *>(&lsap_reg_kernel<CT, 512, 8>);
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+        if (wide)
+            lsap_reg_kernel<CT, 1024, 4><<<dim3((unsigned)n_problems), dim3(1024), lds, s>>>(a);
+        else
+            lsap_reg_kernel<CT, 512, 8><<<dim3((unsigned)n_problems), dim3(512), lds, s>>>(a);
+    }
     // one workgroup per problem: 256 threads (8 batched columns per thread) up to
     // lsap_mid_max_cols long-side columns, 1024 threads (4 per thread) above.
     // MI355X: 4096 x 64 problems 4.00 vs 4.36 ms per 1000 with 256 threads;
@@ -1124,7 +1394,8 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
                col_ind_dev, status_dev, 0, 0, 0,
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
-                   ~(uintptr_t)255)};   // at or after the per-problem regions (all 256-aligned)
+                   ~(uintptr_t)255),   // at or after the per-problem regions (all 256-aligned)
+               0, 0, 0, 0, 0};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (cost_dtype == MVM_F64)
         return lsap_launch<double>(a, n_problems, sync_bytes, long_min, long_max, o, s);

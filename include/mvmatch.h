@@ -109,6 +109,11 @@ typedef struct mvm_options {
                                        with 256 threads (1024 above) */
     int32_t lsap_mid_max_cols;      /* 0 default (8192): workspace-state long sides
                                        up to this with 256 threads (1024 above) */
+    int32_t lsap_reg_max_cols;      /* 0 default (4096); -1 off: long sides up to this
+                                       (short sides <= 1024) in one workgroup with the
+                                       column state in registers (ABI 3) */
+    int32_t lsap_reg_threads;       /* 0 default (512 threads, 8 columns each); 1024
+                                       (4 each) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

@@ -24,19 +24,23 @@ def _batched(cuda, mats, options=None, dtype=np.float32):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-@pytest.fixture(params=["default", "lds", "workgroup", "workgroup256", "multi"])
+@pytest.fixture(params=["default", "reg", "reg1024", "lds", "workgroup", "workgroup256", "multi"])
 def lsap_path(request):
     """mvm_options of each assignment kernel class.  default: long sides <=
-    1024 one problem per wave, up to 4096 one workgroup with the column state
-    in LDS, larger ones split over co-resident workgroups when the batch
-    leaves room; lds: every problem of <= 4096 in the LDS-state workgroup;
-    workgroup: one 1024-thread workgroup per problem with the state in the
-    workspace; workgroup256: the same with 256 threads; multi: every problem
-    split over 4 workgroups."""
+    1024 one problem per wave, up to 4096 (short sides <= 1024) one workgroup
+    with the column state in registers, larger ones split over co-resident
+    workgroups when the batch leaves room, else one workgroup with the state
+    in LDS or the workspace; reg / reg1024: every problem of <= 4096 in the
+    register-state workgroup (512 / 1024 threads); lds: every problem of <=
+    4096 in the LDS-state workgroup; workgroup: one 1024-thread workgroup per
+    problem with the state in the workspace; workgroup256: the same with 256
+    threads; multi: every problem split over 4 workgroups."""
     off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1}
-    return {"default": None, "lds": off,
-            "workgroup": dict(off, lsap_lds_max_cols=-1),
-            "workgroup256": dict(off, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
+    noreg = dict(off, lsap_reg_max_cols=-1)
+    return {"default": None, "reg": off, "reg1024": dict(off, lsap_reg_threads=1024),
+            "lds": noreg,
+            "workgroup": dict(noreg, lsap_lds_max_cols=-1),
+            "workgroup256": dict(noreg, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
             "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4}}[request.param]
 
 
@@ -45,7 +49,8 @@ def test_random_shapes_and_ties_batched(cuda, lsap_path):
     mats = []
     for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0),
                   (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70),
-                  (4096, 6), (6, 4096), (2500, 11), (4097, 3), (513, 7), (768, 5), (5, 768), (769, 4)]:
+                  (4096, 6), (6, 4096), (2500, 11), (4097, 3), (513, 7), (768, 5), (5, 768), (769, 4),
+                  (1025, 2), (4096, 64), (1100, 1100), (1030, 1025)]:
         for trial in range(4):
             c = rng.normal(size=shape).astype(np.float32)
             if trial == 1:

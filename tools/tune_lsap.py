@@ -11,10 +11,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bpc_baseline_amd import ops  # noqa: E402
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
-OFF = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1}
+OFF = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_reg_max_cols": -1}
 VARIANTS = {"default": {},
             "wave": {"lsap_multi_g": -1},
             "multi": {"lsap_wave_max_cols": -1},
+            "reg": {"lsap_wave_max_cols": -1, "lsap_multi_g": -1},
+            "reg1024": {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_reg_threads": 1024},
             "lds": OFF,
             "lds1024": dict(OFF, lsap_lds_small_cols=-1),
             "lds256": dict(OFF, lsap_lds_small_cols=4096),
@@ -25,7 +27,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=1000)
 ap.add_argument("--dets", type=int, default=64)
 ap.add_argument("--rounds", type=int, default=3)
-ap.add_argument("--variants", default="default,lds,wg256,wg1024")
+ap.add_argument("--variants", default="default,reg,reg1024,lds")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 b = make_scenes(args.scenes, 3, args.dets, seed=1)
