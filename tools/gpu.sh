@@ -19,7 +19,7 @@ mkdir -p "$O"
 LIMIT=${LIMIT:-420}
 task=$1; shift || true
 
-fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -25 "$2"; exit 1; }
+fail() { echo "FAIL: $1"; [ -f "$2" ] && tail -n 25 "$2"; exit 1; }
 
 case "$task" in
 check)
