@@ -184,7 +184,11 @@ class LsapSlot:
         self.stage = _Staging([("dims", np.int64, 2), ("ws_offs", np.int64, 2),
                                ("out_offs", np.int64, 2), ("cost_offs", np.int64, 1),
                                ("cost", self.np_dtype, rcap * ccap)], dev)
-        self.ws_capacity = self._plan(rcap, ccap)
+        # the workspace layout depends on the shape's regime (a tall matrix
+        # keeps a transposed copy) and grows with the dims inside a regime:
+        # the capacity is the larger of the two regimes' largest shapes
+        self.ws_capacity = max(self._plan(min(rcap, ccap), ccap),
+                               self._plan(rcap, min(ccap, rcap - 1)) if rcap > 1 else 0)
         self.workspace = torch.empty(max(self.ws_capacity, 16), dtype=torch.uint8, device=dev)
         k = min(rcap, ccap)
         # outputs packed as [row_ind (k) | col_ind (k) | status (int32 in one int64 slot)]

@@ -503,3 +503,23 @@ def test_rig_workers_equal_rig_matrices():
             Fr, Pr = rig_matrices(Ks, RTs)
             assert np.array_equal(F.view(np.int64), Fr.view(np.int64)), k
             assert np.array_equal(P.view(np.int64), Pr.view(np.int64)), k
+
+
+def test_lsap_slot_capacity_covers_every_shape():
+    """A capacity-class assignment slot's workspace covers every shape of its
+    class, tall (transposed copy) and wide alike (mvm_lsap_plan_ex sizes)."""
+    import ctypes
+    from bpc_baseline_amd import _native
+    lib = _native.load()
+
+    def plan(r, c):
+        ws = np.zeros(2, np.int64)
+        out = np.zeros(2, np.int64)
+        ra, ca = np.array([r], np.int64), np.array([c], np.int64)
+        return lib.mvm_lsap_plan_ex(1, ra.ctypes.data, ca.ctypes.data, _native.MVM_F32,
+                                    ws.ctypes.data, out.ctypes.data)
+
+    for rcap, ccap in ((8, 8), (64, 8), (8, 64), (512, 64), (16, 16)):
+        cap = max(plan(min(rcap, ccap), ccap), plan(rcap, min(ccap, rcap - 1)) if rcap > 1 else 0)
+        worst = max(plan(r, c) for r in range(1, rcap + 1) for c in range(1, ccap + 1))
+        assert worst <= cap, (rcap, ccap, worst, cap)
