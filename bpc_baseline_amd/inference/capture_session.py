@@ -138,11 +138,11 @@ class CubeSlot:
         self.dev = dev
 
     def run(self, views, Fs, pts: Optional[torch.Tensor] = None,
-            cam_offs: Optional[torch.Tensor] = None) -> np.ndarray:
+            cam_offs: Optional[torch.Tensor] = None, counts=None) -> np.ndarray:
         """-> a fresh float32 (N, M, P) array (owned by the caller).  ``pts`` /
-        ``cam_offs``: device centroids and offsets of packed detections (then
-        ``views`` only gives the counts)."""
-        N, M, P = (len(v) for v in views)
+        ``cam_offs``: device centroids and offsets of packed detections, with
+        ``counts`` = (N, M, P) (``views`` is then not read)."""
+        N, M, P = (int(c) for c in counts) if counts is not None else (len(v) for v in views)
         st = self.stage
         if pts is None:
             o = 0

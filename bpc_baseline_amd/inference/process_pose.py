@@ -127,7 +127,7 @@ def _packed_cube(det: PackedDetections, F12, F13, F23) -> np.ndarray:
     (only F travels host -> device; capture_session's cached slot)."""
     N, M, P = (int(c) for c in np.diff(det.cam_offs_host[:4]))
     slot = cube_slot(N, M, P, det.pts.device)
-    return slot.run(None, (F12, F13, F23), pts=det.pts, cam_offs=det.cam_offs[:4])
+    return slot.run(None, (F12, F13, F23), pts=det.pts, cam_offs=det.cam_offs[:4], counts=(N, M, P))
 
 
 def match_detections(capture, detections: Dict[int, list], params=None, *,
