@@ -104,25 +104,26 @@ __device__ __forceinline__ void row_fast(const ColRegs &c, double rl0, double rl
 template <bool ARGMIN>
 __device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, double rl1,
                                                  double rl2, double rx, double ry, float *drow,
-                                                 int jbase, Best &best) {
+                                                 int jbase, Best &best, int lim) {
 #pragma unroll
     for (int q = 0; q < kColsPerLane; ++q) {
         const double d1 = __builtin_fma(c.l1[q], ry, c.l0[q] * rx) + c.l2[q];
         const double d2 = __builtin_fma(rl1, c.y[q], rl0 * c.x[q]) + rl2;
         const float v = (float)half_for_f32(__builtin_fabs(d1) + __builtin_fabs(d2));
-        if (c.state[q] != kNone) {
-            if (drow) drow[jbase + kWave * q] = v;
-            if (ARGMIN) best_update_fast(best, v, jbase + kWave * q);
-        }
+        const int j = jbase + kWave * q;
+        if (drow && j < lim) drow[j] = v;    // a pitched row's padding: +inf (pad lines)
+        if (ARGMIN && c.state[q] != kNone) best_update_fast(best, v, j);
     }
 }
 
 // Generic row: degenerate lines (9999 sentinel), non-finite or huge values,
 // tails, unaligned rows, no output buffer.  Column of slot q: jbase + q*jstep.
+// Columns past the view but inside the row's pitch (j < lim) are stored too:
+// their pad lines give +inf, as the other paths write.
 template <bool ARGMIN, typename OutT>
 __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, bool rdeg, OutT *drow, int jbase,
-                                         int jstep, Best &best) {
+                                         int jstep, Best &best, int lim) {
 #pragma unroll
     for (int q = 0; q < kColsPerLane; ++q) {
         double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);
@@ -131,7 +132,8 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
         const double e = 0.5 * (d1 + d2);                                            // :28
         const bool valid = c.state[q] != kNone;
         const int j = jbase + q * jstep;
-        if (drow && valid) drow[j] = (OutT)e;   // default policy: L2 merges partial lines
+        // j < lim: the view's columns and a pitched row's padding (lim = ld >= n_b)
+        if (drow && j < lim) drow[j] = (OutT)e;   // default policy: L2 merges partial lines
         if (ARGMIN && valid) best_update_safe(best, (float)e, j);
     }
 }
@@ -388,8 +390,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
         int xw, grow0, nrows;
         group_rows(g, xw, grow0, nrows);
         double(*rowp)[6] = s_row[wave] + (pre ? g * RPW : 0);   // this group's slots
-        if (!pre && lane < RPW)   // row lines of this wave's group (wave-private LDS slots)
-            put_row_line(lane, xw, lane, nrows);
+        if (!pre && lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
+            int lz = lane;          // fresh per group: its LDS address is not hoisted and spilled
+            __asm__ volatile("" : "+v"(lz));
+            put_row_line(lz, xw, lz, nrows);
+        }
         // the same wave reads them back (LDS executes one wave's ops in order)
         const bool rows_fast =
             (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
@@ -535,7 +540,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                                                  rowp[r][4],
                                                  dbase ? reinterpret_cast<float *>(dbase + (int64_t)(grow0 + r) * ld)
                                                        : nullptr,
-                                                 jbase, best[r]);
+                                                 jbase, best[r], lim);
                     }
                 } else if (tail && vec_ok && rows_fast && __all(clean_m)) {   // aligned tail chunk
                     const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
@@ -578,7 +583,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                                                   (int)rowp[r][5]) == (int)kDeg;
                             row_safe<ARGMIN>(c, rowp[r][0], rowp[r][1],
                                              rowp[r][2], rowp[r][3],
-                                             rowp[r][4], rdeg, drow, jbase, jstep, best[r]);
+                                             rowp[r][4], rdeg, drow, jbase, jstep, best[r], lim);
                         }
                     }
                 }

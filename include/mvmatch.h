@@ -157,8 +157,8 @@ int mvm_pairwise_residual_argmin_ex(const double *pts_dev, const int64_t *cam_of
  *   dist_dev[dist_offs_dev[s*P + p] + i*ld],  ld = roundup(n_b, row_align),
  * so with row_align 32 (and matrix offsets that are multiples of 32) every
  * row starts on a 128-byte line and every store of a ragged view writes whole
- * lines.  Columns n_b .. ld-1 of a row are padding: +inf where the kernel
- * writes them, otherwise unspecified.  row_align is a power of two in
+ * lines.  Columns n_b .. ld-1 of a row are padding and hold +inf.  row_align
+ * is a power of two in
  * [1, 256]; 1 is the unpitched layout of mvm_pairwise_residual_argmin_ex.
  * The caller sizes dist_dev and dist_offs_dev with the pitched sizes n_a*ld.
  */
