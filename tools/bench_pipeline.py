@@ -78,7 +78,7 @@ def main():
     torch.cuda.synchronize()
     dt_cached = (time.perf_counter() - t0) / args.steps
     # the same batches through the pipelined stream (host F/P of batch b+1
-    # on a worker thread while batch b runs on the device)
+    # in worker processes while batch b runs on the device)
     batches = [(boxes, conf, cls, offs, b.Ks, b.RTs)] * args.steps
     for _ in match_capture_stream(batches[:2]):
         pass
@@ -88,6 +88,13 @@ def main():
         res_stream = r
     torch.cuda.synchronize()
     dt_stream = (time.perf_counter() - t0) / args.steps
+    # the same stream with F/P computed inline (no worker processes)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for r in match_capture_stream(batches, rig_workers=0):
+        pass
+    torch.cuda.synchronize()
+    dt_inline = (time.perf_counter() - t0) / args.steps
     assert np.array_equal(res_stream.count, res.count)
     ms, mr = res_stream.match.cpu().numpy(), res.match.cpu().numpy()
     for s in range(args.captures):   # rows past count[s] are unused capacity
@@ -121,8 +128,10 @@ def main():
         "matches": int(res.count.sum()), "parity_checked": len(check),
         "stage_ms_synchronised": stages,
         "stream": {"value": args.captures / dt_stream, "ms_per_batch": dt_stream * 1e3,
-                   "note": "match_capture_stream: host F/P of the next batch overlapped with "
-                           "this batch's device chain"},
+                   "inline_ms_per_batch": dt_inline * 1e3,
+                   "note": "match_capture_stream: host F/P of the next batch computed by 3 worker "
+                           "processes (shared memory) while this batch's device chain runs; "
+                           "inline: the same stream with F/P in the main process"},
         "static_rig": {"value": args.captures / dt_cached, "ms_per_batch": dt_cached * 1e3,
                        "note": "F and P computed once and passed in (fixed camera rig)"},
         "cpu_chain": {"value": cpu, "unit": "captures/s", "cores": 1, "kind": "port",
