@@ -8,6 +8,11 @@
 #   bash tools/gpu.sh pmc W [bench args]      FETCH_SIZE and WRITE_SIZE, one pass each
 #   bash tools/gpu.sh sq "PMC LIST" TOOL [args]  one --pmc pass over a tools/ script
 #   bash tools/gpu.sh py TOOL [args]          a tools/ script (or bench.py) under a time limit
+#   AB_LIBS="a.so b.so" bash tools/gpu.sh ab CMD...
+#                                             in-tree library builds (MVM_LIB_PATH) timed by
+#                                             CMD in alternating processes, AB_ROUNDS rounds
+#                                             (same-buffer A/B in one process:
+#                                             tools/ab_same_buffers.py)
 #
 # Output goes to gpurun_out/$RUN/ (default gpurun_out/run).  Every GPU step has
 # its own time limit; a failing step ends the script with its status.
@@ -62,6 +67,13 @@ py)
   timeout -k 10 "$LIMIT" python -u "$T" "$@" > "$O/$N.out" 2> "$O/$N.err" \
     || fail "$T" "$O/$N.err"
   tail -40 "$O/$N.out" ;;
+ab)
+  for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
+    for lib in $AB_LIBS; do
+      echo "== $lib (round $rnd)"
+      MVM_LIB_PATH=$lib timeout -k 10 200 "$@" 2>&1 | grep -v amdgpu.ids || exit 1
+    done
+  done ;;
 *)
   echo "unknown task '$task'"; exit 2 ;;
 esac
