@@ -627,9 +627,15 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
             } else if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
                 uint32_t mk;
                 int32_t mi;
-                wave_argmin8_transposed(key, idx, lane, mk, mi);
-                if (lane < nrows) {
-                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                // the lane id as a fresh value: the row address below is then
+                // computed here, not hoisted out of the tile loop and spilled
+                // (its reload after the row stores waited for all of them:
+                // vmcnt is in order)
+                int lz = lane;
+                __asm__ volatile("" : "+v"(lz));
+                wave_argmin8_transposed(key, idx, lz, mk, mi);
+                if (lz < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + lz;
                     if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
                     if (args.minval) args.minval[row] = value_of_key(mk);
                 }
@@ -642,7 +648,9 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     imin[r] = 0;
                     if (r < nrows) wave_argmin(key[r], idx[r], kmin[r], imin[r]);
                 }
-                store_row_results<kCubeRPW>(kmin, imin, nrows, lane, args.argmin, args.minval,
+                int lz = lane;   // fresh per row group (see above)
+                __asm__ volatile("" : "+v"(lz));
+                store_row_results<kCubeRPW>(kmin, imin, nrows, lz, args.argmin, args.minval,
                                             roff + (int64_t)i * M + j0);
             }
         }
