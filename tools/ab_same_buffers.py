@@ -29,6 +29,7 @@ ap.add_argument("--workload", choices=["cube", "c3", "c2"], default="cube")
 ap.add_argument("--buffers", type=int, default=6)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--scenes", type=int, default=None, help="scenes per launch (cube 250, c3 1000)")
+ap.add_argument("--dets", type=int, default=256, help="detections per view (cube)")
 ap.add_argument("--alloc", default=None,
                 help="comma list of buffer kinds instead of --buffers torch buffers: "
                      "torch | vmm:MB (HIP VMM API: physical chunks of MB MiB mapped contiguously)")
@@ -99,7 +100,7 @@ for path in args.libs.split(","):
 dev = torch.device("cuda", 0)
 P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
 if args.workload == "cube":
-    b = make_scenes(args.scenes or 250, 3, 256, seed=0)
+    b = make_scenes(args.scenes or 250, 3, args.dets, seed=0)
     plan = ops.TripletPlan(b.cam_offs, b.n_scenes, device=dev)
     n_out = plan.n_cube
 else:
