@@ -59,6 +59,10 @@ struct LsapArgs {
     int32_t reg_max_cols;       // long sides in (wave_max_cols, this] with short sides <=
                                 // kRegMaxShort: lsap_reg_kernel (column state in VGPRs)
     int32_t reg_nc_cap, reg_nr_cap;   // its dynamic LDS sizing (columns, rows)
+    int32_t mreg_g;             // > 0: long sides in (mreg_lo, mreg_max_cols] with short sides
+                                // <= kRegMaxShort run in lsap_mreg_kernel, mreg_g workgroups each
+    int32_t mreg_slots;         // ... in this many co-resident groups of workgroups
+    int32_t mreg_lo, mreg_max_cols, mreg_nr_cap;
 };
 
 // lsap_reg_kernel's class: short sides up to this (its row state is in LDS)
@@ -69,6 +73,11 @@ __device__ __forceinline__ bool in_reg_class(const LsapArgs &a, int64_t R, int64
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
     return a.reg_max_cols > 0 && lng > a.wave_max_cols && lng <= a.reg_max_cols &&
            sht <= kRegMaxShort;
+}
+
+__device__ __forceinline__ bool in_mreg_class(const LsapArgs &a, int64_t R, int64_t K) {
+    const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
+    return a.mreg_g > 0 && lng > a.mreg_lo && lng <= a.mreg_max_cols && sht > 0 && sht <= kRegMaxShort;
 }
 
 // Column state of lsap_kernel<.., true> in LDS: spc, v (f64), path, row4col,
@@ -183,6 +192,7 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     if ((R > K ? R : K) <= a.wave_max_cols) return;   // solved by lsap_wave_kernel
     if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
     if (in_reg_class(a, R, K)) return;                 // solved by lsap_reg_kernel
+    if (in_mreg_class(a, R, K)) return;                // solved by lsap_mreg_kernel
     const int64_t longside = R > K ? R : K;
     // class of the problem: LDS state with 256 threads (long side <= lds_small)
     // or 1024 threads, then workspace state with 256 or 1024 threads
@@ -682,7 +692,8 @@ __device__ __forceinline__ bool validate_transpose(const LsapArgs &a, const CT *
 // agent-scope fences around the barrier.  Barrier waits are bounded: a
 // timeout reports status 3 instead of hanging.
 constexpr int kMultiMaxG = 16;
-constexpr size_t kSyncBytes = 1280;     // counter + flags + 2 x kMultiMaxG records
+constexpr size_t kSyncBytes = 2304;     // lsap_multi_kernel: counter + flags + 2 x kMultiMaxG
+                                        // records; lsap_mreg_kernel: flag + 2 x kMultiMaxG x 8 granules
 
 struct MRed {
     double m;
@@ -958,6 +969,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_multi_kernel(LsapArgs a, in
     const int t = threadIdx.x, lane = t % 64, wave = t / 64;
     const int64_t R = a.dims[2 * p], K = a.dims[2 * p + 1];
     if (R == 0 || K == 0 || (R > K ? R : K) <= a.wave_max_cols) return;
+    if (in_mreg_class(a, R, K)) return;                // solved by lsap_mreg_kernel
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const int64_t c0 = nc * g / G, c1 = nc * (g + 1) / G;   // owned columns [c0, c1)
@@ -1179,6 +1191,527 @@ timeout:
     if (g == 0 && t == 0) a.status[p] = 3;
 }
 
+// ------------------ G workgroups per problem, column state in VGPRs ----
+// The flattened cubes of 65-256 detections per view (8,192 .. 65,536 x 256):
+// lsap_reg_kernel's register layout spread over G co-resident workgroups of
+// 512 threads x 8 columns (cooperative launch), persistent over the batch:
+// slot s (G workgroups on one XCD) solves the class's problems s, s + slots,
+// ...  What the sequential algorithm reads across columns reaches every
+// workgroup through ONE exchange per Dijkstra step: each workgroup publishes
+// its best candidate record -- keys (scan position << 16 | column), plus the
+// row4col and the path STEP of its candidate columns -- and after one
+// barrier every wave combines the G records in the same order, so the
+// decisions are uniform over the slot.  Each workgroup keeps the step lists
+// (row, column, path step, minimum) of the search, so both the row-dual
+// update (u[i_k] += minVal - m_(k-1): the chosen column's spc IS the step's
+// minimum) and the augmentation walk (path[j_k] = i_(ps_k), col4row[i_s] =
+// j_(s-1)) are local replays over replicated row duals and col4row in LDS:
+// no global row state, no per-search barrier, no path array in memory.
+// Keys: positions and columns below 65,536.  `first` none is ~0u (column 0
+// is the only one that can sit at position 65,535); `last_free` none is 0
+// (key 0 as the last free minimum is also the first minimum and free: the
+// same column and sink either way).
+constexpr int kMregNT = 512, kMregK = 8;
+constexpr int kMregCols = kMregNT * kMregK;              // columns per workgroup
+constexpr int kMregMaxCols = kMultiMaxG * kMregCols;     // 65,536
+
+struct URed {
+    double m;
+    uint32_t first, last_free;
+};
+
+__device__ __forceinline__ URed ured_combine(URed a, const URed &b) {
+    if (b.m < a.m) return b;
+    if (a.m < b.m) return a;
+    a.first = b.first < a.first ? b.first : a.first;
+    a.last_free = b.last_free > a.last_free ? b.last_free : a.last_free;
+    return a;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp64(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), CTRL,
+                                               0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, CTRL, 0xF, 0xF, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ URed ured_dpp_step(URed r) {
+    URed o{dpp64<CTRL>(r.m), dpp32<CTRL>(r.first), dpp32<CTRL>(r.last_free)};
+    return ured_combine(r, o);
+}
+
+__device__ __forceinline__ URed ured_readlane(const URed &r, int l) {
+    const uint64_t mb = (uint64_t)__double_as_longlong(r.m);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)mb, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(mb >> 32), l);
+    return URed{__longlong_as_double((long long)(((uint64_t)hi << 32) | lo)),
+                (uint32_t)__builtin_amdgcn_readlane((int)r.first, l),
+                (uint32_t)__builtin_amdgcn_readlane((int)r.last_free, l)};
+}
+
+__device__ __forceinline__ URed ured_wave(URed r) {
+    r = ured_dpp_step<0xB1>(r);
+    r = ured_dpp_step<0x4E>(r);
+    r = ured_dpp_step<0x141>(r);
+    r = ured_dpp_step<0x140>(r);
+    URed a = ured_readlane(r, 0);
+    a = ured_combine(a, ured_readlane(r, 16));
+    a = ured_combine(a, ured_readlane(r, 32));
+    return ured_combine(a, ured_readlane(r, 48));
+}
+
+// one workgroup's record; ps = path step of `first` | of `last_free` << 16
+struct alignas(16) XRed {
+    double m;
+    uint32_t first, last_free;
+    int32_t first_r4;
+    uint32_t ps;
+    uint32_t pad[2];
+};
+
+__device__ __forceinline__ XRed xred_combine(XRed a, const XRed &b) {
+    if (b.m < a.m) return b;
+    if (a.m < b.m) return a;
+    if (b.first < a.first) {
+        a.first = b.first;
+        a.first_r4 = b.first_r4;
+        a.ps = (a.ps & 0xFFFF0000u) | (b.ps & 0xFFFFu);
+    }
+    if (b.last_free > a.last_free) {
+        a.last_free = b.last_free;
+        a.ps = (a.ps & 0xFFFFu) | (b.ps & 0xFFFF0000u);
+    }
+    return a;
+}
+
+template <int CTRL>
+__device__ __forceinline__ XRed xred_dpp_step(XRed r) {
+    XRed o = r;
+    o.m = dpp64<CTRL>(r.m);
+    o.first = dpp32<CTRL>(r.first);
+    o.last_free = dpp32<CTRL>(r.last_free);
+    o.first_r4 = (int32_t)dpp32<CTRL>((uint32_t)r.first_r4);
+    o.ps = dpp32<CTRL>(r.ps);
+    return xred_combine(r, o);
+}
+
+// Records travel as tagged granules (MI355X_MICROARCH.md, hand-off R2): each
+// 32-bit field is one naturally aligned 8-byte {tag = exchange number, value}
+// written by one relaxed agent-scope (sc1, write-through) store; readers poll
+// with sc1 loads until every tag matches.  The data is its own flag: no
+// counter, no release (L2 write-back) or acquire (L1 invalidate) fence.  Two
+// buffers alternate: a workgroup republishes a buffer only after reading the
+// records of the exchange in between, which every other workgroup publishes
+// only after reading this buffer's.
+struct XSync {
+    int flag;          // 3: a workgroup timed out waiting for the others
+    int pad[63];
+    unsigned long long gran[2][kMultiMaxG][8];
+};
+static_assert(sizeof(XSync) <= kSyncBytes, "sync block too large");
+constexpr int kXFields = 6;    // m (2 words), first, last_free, first_r4, ps
+constexpr long kSpinLimit = 1L << 24;
+
+// lanes < G of a wave: wait for and read workgroup `lane`'s record of exchange tag
+__device__ __forceinline__ bool xsync_read(XSync *sb, int par, int lane, int G, uint32_t tag,
+                                           uint32_t (&v)[kXFields]) {
+    bool ok = true;
+    if (lane < G) {
+        unsigned long long *q = &sb->gran[par][lane][0];
+        for (long spins = 0;; ++spins) {
+            bool all = true;
+#pragma unroll
+            for (int e = 0; e < kXFields; ++e) {
+                const unsigned long long x = __hip_atomic_load(q + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                v[e] = (uint32_t)x;
+                all &= (uint32_t)(x >> 32) == tag;
+            }
+            if (all) break;
+            if (spins > kSpinLimit ||
+                __hip_atomic_load(&sb->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 3) {
+                atomicExch(&sb->flag, 3);
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return __ballot(!ok) == 0;
+}
+
+// lanes e < kXFields of ONE wave: publish field e (one store instruction)
+__device__ __forceinline__ void xsync_publish(XSync *sb, int par, int g, int lane, uint32_t tag, uint32_t val) {
+    if (lane < kXFields)
+        __hip_atomic_store(&sb->gran[par][g][lane], ((unsigned long long)tag << 32) | val, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// dynamic LDS of lsap_mreg_kernel for short sides up to cap
+__host__ __device__ constexpr size_t mreg_lds_bytes(int cap) {
+    return (size_t)kMregCols * 4 + (size_t)cap * 8 + (size_t)(cap + 1) * 8 + (size_t)cap * 4 +
+           (size_t)(cap + 1) * 8 + (size_t)(cap + 1) * 2 + (size_t)kMregCols * 2;
+}
+
+// C0 rows [r_lo, r_hi) of ncols columns (row-major) -> Ctw[c * ld_out + r]
+// through LDS tiles, D tiles' loads in flight at once (the one-tile loop waits
+// a full memory latency per 16 KB tile: 0.85 ms of a 256^3 problem on 16
+// workgroups).  Returns this thread's invalid-entry flag (NaN / -inf).
+template <typename CT, int NT, int D>
+__device__ __forceinline__ int transpose_rows(const CT *C0, CT *Ctw, int r_lo, int r_hi, int ncols,
+                                              int64_t ld_out, CT (*s_tile)[kTile * 4 / sizeof(CT) + 1]) {
+    constexpr int kT = kTile * 4 / (int)sizeof(CT), E = kT * kT / NT;
+    static_assert(E * NT == kT * kT, "a tile is E elements per thread");
+    const int t = threadIdx.x;
+    const int ntc = (ncols + kT - 1) / kT, ntiles = (r_hi - r_lo + kT - 1) / kT * ntc;
+    int bad = 0;
+    for (int tb = 0; tb < ntiles; tb += D) {
+        CT val[D][E];
+#pragma unroll
+        for (int d = 0; d < D; ++d) {                        // all D tiles' loads first
+            const int tt = tb + d;
+            const int r0 = r_lo + (tt / ntc) * kT, cc0 = (tt % ntc) * kT;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int x = t + NT * e, rr = x / kT, cc = x % kT;
+                val[d][e] = tt < ntiles && r0 + rr < r_hi && cc0 + cc < ncols
+                                ? C0[(int64_t)(r0 + rr) * ncols + cc0 + cc] : (CT)0;
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const int tt = tb + d;
+            if (tt >= ntiles) break;                         // uniform
+            const int r0 = r_lo + (tt / ntc) * kT, cc0 = (tt % ntc) * kT;
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int x = t + NT * e, rr = x / kT, cc = x % kT;
+                bad |= (val[d][e] != val[d][e]) || (val[d][e] == -INFINITY);
+                s_tile[rr][cc] = val[d][e];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int e = 0; e < E; ++e) {
+                const int x = t + NT * e, cc = x / kT, rr = x % kT;
+                if (r0 + rr < r_hi && cc0 + cc < ncols) Ctw[(int64_t)(cc0 + cc) * ld_out + r0 + rr] = s_tile[rr][cc];
+            }
+            __syncthreads();
+        }
+    }
+    return bad;
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32_t n) {
+    constexpr int NT = kMregNT, K = kMregK, kNW = NT / 64;
+    constexpr int kT = kTile * 4 / (int)sizeof(CT);
+    __shared__ CT s_tile[kT][kT + 1];
+    __shared__ URed s_rec[kNW];
+    __shared__ int s_flag;
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+
+    const int G = a.mreg_g, slots = a.mreg_slots, cap = a.mreg_nr_cap;
+    // a slot's G workgroups on one XCD (dispatch round-robins workgroups over the 8)
+    const int b = blockIdx.x, xcd = b % 8, qg = b / 8;
+    const int slot = xcd + 8 * (qg / G), g = qg % G;
+    if (slot >= slots) return;
+    const int t = threadIdx.x, lane = t % 64, wave = t / 64;
+    // LDS: per owned column row4col and path step; replicated row duals and
+    // col4row; the search's step lists (row, column, path step, minimum)
+    int32_t *s_r4c = reinterpret_cast<int32_t *>(s_dyn);   // [kMregCols]
+    double *s_u = reinterpret_cast<double *>(s_r4c + kMregCols);   // [cap]
+    double *s_m = s_u + cap;                                 // [cap + 1]
+    int32_t *c4r = reinterpret_cast<int32_t *>(s_m + cap + 1);   // [cap]
+    int32_t *s_i = c4r + cap;                                // [cap + 1]
+    int32_t *s_j = s_i + cap + 1;                            // [cap + 1]
+    uint16_t *s_pk = reinterpret_cast<uint16_t *>(s_j + cap + 1);   // [cap + 1]
+    uint16_t *s_ps = s_pk + cap + 1;                         // [kMregCols]
+    XSync *sb = reinterpret_cast<XSync *>(a.sync + (size_t)slot * kSyncBytes);
+    uint32_t gen = 0;                                        // exchanges so far (the tags)
+    int par = 0, kth = 0;
+#ifdef MVM_LSAP_PROF   // diagnostic build only: phase times of slot 0's workgroup 0 (100 MHz clock)
+    uint64_t pf[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pt0 = 0, pt = 0;
+    int pst = 0;
+#define MREG_PT(k) do { if (t == 0) { const uint64_t n_ = wall_clock64(); pf[k] += n_ - pt; pt = n_; } } while (0)
+#else
+#define MREG_PT(k) do { } while (0)
+#endif
+
+    for (int p = 0; p < n; ++p) {
+        const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+        if (!in_mreg_class(a, R, Kd)) continue;
+        if (kth++ % slots != slot) continue;
+        const bool transpose = Kd < R;
+        const int nr = (int)(transpose ? Kd : R), nc = (int)(transpose ? R : Kd);
+        const int c0 = (int)((int64_t)nc * g / G), c1 = (int)((int64_t)nc * (g + 1) / G);
+        const int own = c1 - c0;
+        const Layout L = lsap_layout(nr, nc, transpose, sizeof(CT));
+        unsigned char *w = a.ws + a.ws_offs[p];
+        const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
+        const CT *Ct = transpose ? reinterpret_cast<const CT *>(w + L.ct) : C0;
+
+        // ---- validate and transpose the owned columns; init --------------
+        __syncthreads();                                     // the previous problem's output is read
+#ifdef MVM_LSAP_PROF
+        if (t == 0) { pt0 = pt = wall_clock64(); pst = 0; for (int z = 0; z < 8; ++z) pf[z] = 0; }
+#endif
+        if (t == 0) s_flag = 0;
+        __syncthreads();
+        int bad = 0;
+        if (transpose) {                                     // rows of C0 = owned columns
+            bad = transpose_rows<CT, NT, (sizeof(CT) == 4 ? 4 : 8)>(C0, reinterpret_cast<CT *>(w + L.ct), c0, c1, nr, nc, s_tile);
+        } else {
+            for (int i = 0; i < nr; ++i)
+                for (int j = c0 + t; j < c1; j += NT) {
+                    const CT val = C0[(int64_t)i * nc + j];
+                    bad |= (val != val) || (val == -INFINITY);
+                }
+        }
+        if (bad) atomicOr(&s_flag, 1);
+        for (int i = t; i < nr; i += NT) {
+            s_u[i] = 0.0;
+            c4r[i] = -1;
+        }
+        for (int jl = t; jl < kMregCols; jl += NT) s_r4c[jl] = -1;
+        double spc[K], v[K];
+        int32_t pos[K];
+        uint32_t freem = 0;                                  // bit q: column c0 + t + NT q has no row
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            v[q] = 0.0;
+            freem |= t + NT * q < own ? 1u << q : 0u;
+        }
+        __syncthreads();
+        {                                                    // any workgroup's entries invalid?
+            const uint32_t tag = ++gen;
+            if (wave == 0) xsync_publish(sb, par, g, lane, tag, (uint32_t)s_flag);
+            uint32_t f[kXFields];
+            if (!xsync_read(sb, par, lane, G, tag, f)) goto timeout;
+            par ^= 1;
+            if (__ballot(lane < G && f[0] != 0u)) {
+                if (g == 0 && t == 0) a.status[p] = 1;
+                continue;
+            }
+        }
+
+        // ---- one shortest augmenting path per short-side row -------------
+        MREG_PT(0);                                          // validate + transpose + first exchange
+        for (int cur = 0; cur < nr; ++cur) {
+            uint32_t insc = 0;
+            // per-search and per-step uniforms are laundered through an SGPR so
+            // their per-lane derivatives are recomputed, not held in VGPRs for the
+            // whole problem (that hoisting spilled 8 VGPRs)
+            int base = __builtin_amdgcn_readfirstlane(nc - 1 - c0);
+            asm volatile("" : "+s"(base));
+#pragma unroll
+            for (int q = 0; q < K; ++q) {
+                const int jl = t + NT * q;
+                spc[q] = INFINITY;
+                pos[q] = jl < own ? base - jl : -1;   // reverse column order
+            }
+            int i = cur, nrem = nc, k = 0, sink = -1;
+            double min_val = 0.0;
+            __syncthreads();                                 // the previous row's replay is in place
+            while (true) {
+                const double ui = s_u[i];
+                const CT *Ci = Ct + (int64_t)i * nc + c0;
+                int lim = __builtin_amdgcn_readfirstlane(own > 0 ? own - 1 : 0);   // c0 < nc
+                asm volatile("" : "+s"(lim));
+                CT cq[K];
+#pragma unroll
+                for (int q = 0; q < K; ++q) cq[q] = Ci[min(t + NT * q, lim)];   // all loads first
+                URed best{INFINITY, ~0u, 0u};
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    if (pos[q] < 0) continue;                // visited, or past the owned columns
+                    const int jl = t + NT * q;
+                    const double r = ((min_val + (double)cq[q]) - ui) - v[q];
+                    if (r < spc[q]) {
+                        s_ps[jl] = (uint16_t)k;
+                        spc[q] = r;
+                    }
+                    const double sq = spc[q];
+                    const uint32_t key = ((uint32_t)pos[q] << 16) | (uint32_t)(c0 + jl);
+                    const bool fr = (freem >> q) & 1u;
+                    if (sq < best.m) {
+                        best.m = sq;
+                        best.first = key;
+                        best.last_free = fr ? key : 0u;
+                    } else if (sq == best.m) {
+                        best.first = key < best.first ? key : best.first;
+                        if (fr && key > best.last_free) best.last_free = key;
+                    }
+                }
+                best = ured_wave(best);
+                MREG_PT(1);                                  // row load + scan + wave reduction
+                if (lane == 0) s_rec[wave] = best;
+                __syncthreads();
+                MREG_PT(2);                                  // workgroup barrier
+                const uint32_t tag = ++gen;
+                if (wave == 0) {                             // publish this workgroup's record
+                    URed w{INFINITY, ~0u, 0u};
+                    if (lane < kNW) w = s_rec[lane];
+                    w = ured_dpp_step<0xB1>(w);
+                    w = ured_dpp_step<0x4E>(w);
+                    w = ured_dpp_step<0x141>(w);
+                    w = ured_readlane(w, 0);
+                    uint32_t f_r4 = ~0u, ps = 0u;            // row4col -1 when no candidate
+                    if (w.first != ~0u) {
+                        const int jl = (int)(w.first & 0xFFFFu) - c0;
+                        f_r4 = (uint32_t)s_r4c[jl];
+                        ps = s_ps[jl];
+                    }
+                    if (w.last_free != 0u) ps |= (uint32_t)s_ps[(int)(w.last_free & 0xFFFFu) - c0] << 16;
+                    const uint64_t mb = (uint64_t)__double_as_longlong(w.m);
+                    const uint32_t val = lane == 0 ? (uint32_t)mb : lane == 1 ? (uint32_t)(mb >> 32)
+                                       : lane == 2 ? w.first : lane == 3 ? w.last_free : lane == 4 ? f_r4 : ps;
+                    xsync_publish(sb, par, g, lane, tag, val);
+                }
+                MREG_PT(3);                                  // workgroup record + publish
+                // every wave reads and combines the G records: lane l < G holds record l
+                uint32_t f[kXFields];
+                if (!xsync_read(sb, par, lane, G, tag, f)) goto timeout;
+                MREG_PT(4);                                  // waiting for the slot's records
+#ifdef MVM_LSAP_PROF
+                ++pst;
+#endif
+                XRed r{INFINITY, ~0u, 0u, -1, 0u, {0u, 0u}};
+                if (lane < G) {
+                    r.m = __longlong_as_double((long long)(((uint64_t)f[1] << 32) | f[0]));
+                    r.first = f[2];
+                    r.last_free = f[3];
+                    r.first_r4 = (int32_t)f[4];
+                    r.ps = f[5];
+                }
+                r = xred_dpp_step<0xB1>(r);
+                r = xred_dpp_step<0x4E>(r);
+                if (G > 4) r = xred_dpp_step<0x141>(r);
+                if (G > 8) r = xred_dpp_step<0x140>(r);
+                {
+                    const uint64_t mb = (uint64_t)__double_as_longlong(r.m);
+                    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mb);
+                    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(mb >> 32));
+                    r.m = __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+                    r.first = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.first);
+                    r.last_free = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.last_free);
+                    r.first_r4 = __builtin_amdgcn_readfirstlane(r.first_r4);
+                    r.ps = (uint32_t)__builtin_amdgcn_readfirstlane((int)r.ps);
+                }
+                par ^= 1;
+                if (!(r.m < INFINITY)) break;                // infeasible (uniform over the slot)
+                const bool use_free = r.last_free != 0u;
+                const uint32_t key = use_free ? r.last_free : r.first;
+                const int index = (int)(key >> 16), j = (int)(key & 0xFFFFu);
+                const int r4 = use_free ? -1 : r.first_r4;
+                const int psk = (int)(use_free ? r.ps >> 16 : r.ps & 0xFFFFu);
+                --nrem;
+#pragma unroll
+                for (int q = 0; q < K; ++q) {                // swap-with-last removal, by the owners
+                    if (pos[q] == nrem) pos[q] = index;
+                    if (c0 + t + NT * q == j) {              // (after: last == j leaves j removed)
+                        pos[q] = -1;
+                        insc |= 1u << q;
+                    }
+                }
+                if (t == 0) {
+                    s_i[k] = i;
+                    s_j[k] = j;
+                    s_pk[k] = (uint16_t)psk;
+                    s_m[k] = r.m;
+                }
+                min_val = r.m;
+                if (r4 == -1) {
+                    sink = j;
+                    break;
+                }
+                i = r4;
+                MREG_PT(5);                                  // combine + decision
+                if (++k > nr) {                              // a step list overflow cannot happen
+                    if (t == 0) atomicExch(&sb->flag, 3);
+                    goto timeout;
+                }
+            }
+            if (sink < 0) break;                             // infeasible
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                if ((insc >> q) & 1u) v[q] -= min_val - spc[q];
+            // row duals: u[cur] += minVal; u[i_k] += minVal - spc[col4row[i_k]]
+            // with col4row[i_k] = j_(k-1), whose spc is step k-1's minimum (rows
+            // distinct: one lane each)
+            if (wave == 0)
+                for (int kk = 1 + lane; kk <= k; kk += 64) s_u[s_i[kk]] += min_val - s_m[kk - 1];
+            if (t == 0) {
+                s_u[cur] += min_val;
+                // augment: path[j_kk] = i_s (s = its path step); col4row[i_s] was j_(s-1)
+                int kk = k;
+                while (true) {
+                    const int s = s_pk[kk], i2 = s_i[s], jj = s_j[kk];
+                    c4r[i2] = jj;
+                    if (jj >= c0 && jj < c1) s_r4c[jj - c0] = i2;
+                    if (s == 0) break;
+                    kk = s - 1;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < K; ++q)                      // path columns (all visited) now have rows
+                if ((insc >> q) & 1u) freem &= s_r4c[t + NT * q] == -1 ? ~0u : ~(1u << q);
+            MREG_PT(6);                                      // search end: duals, walk
+        }
+        __syncthreads();
+        MREG_PT(7);
+#ifdef MVM_LSAP_PROF
+        if (t == 0 && g == 0 && slot == 0)
+            printf("mreg p=%d G=%d steps=%d total=%lu prep=%lu scan=%lu wgbar=%lu pub=%lu wait=%lu dec=%lu end=%lu\n",
+                   p, G, pst, (unsigned long)(pt - pt0), (unsigned long)pf[0], (unsigned long)pf[1],
+                   (unsigned long)pf[2], (unsigned long)pf[3], (unsigned long)pf[4], (unsigned long)pf[5],
+                   (unsigned long)pf[6]);
+#endif
+        if (g == 0) {
+            bool feasible = true;
+            for (int r = 0; r < nr; ++r) feasible &= c4r[r] >= 0;   // uniform LDS reads
+            if (!feasible) {
+                if (t == 0) a.status[p] = 2;                 // infeasible
+                continue;
+            }
+            const int64_t o = a.out_offs[p];                 // output pairs in scipy's order
+            if (transpose) {
+                for (int kk = t; kk < nr; kk += NT) {
+                    const int32_t rk = c4r[kk];
+                    int rank = 0;
+                    for (int k2 = 0; k2 < nr; ++k2) rank += c4r[k2] < rk;
+                    a.row_ind[o + rank] = rk;
+                    a.col_ind[o + rank] = kk;
+                }
+            } else {
+                for (int kk = t; kk < nr; kk += NT) {
+                    a.row_ind[o + kk] = kk;
+                    a.col_ind[o + kk] = c4r[kk];
+                }
+            }
+            if (t == 0) a.status[p] = 0;
+        }
+    }
+    return;
+timeout:
+    if (g == 0 && t == 0) {                                  // this and the slot's later problems
+        int idx = 0;
+        for (int p = 0; p < n; ++p) {
+            const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+            if (!in_mreg_class(a, R, Kd)) continue;
+            const int me = idx++;
+            if (me % slots == slot && me >= kth - 1) a.status[p] = 3;
+        }
+    }
+}
+
 // Launch every kernel class of the batch for cost element type CT.
 template <typename CT>
 int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_min,
@@ -1229,6 +1762,48 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
         }
     }
     const bool big = long_max > wave_max;   // anything left for the workgroup kernels
+    int reg_max = o.lsap_reg_max_cols == 0 ? kRegMaxCols : o.lsap_reg_max_cols;
+    reg_max = reg_max < 0 ? 0 : (reg_max > kRegMaxCols ? kRegMaxCols : reg_max);
+    a.reg_max_cols = reg_max > wave_max ? reg_max : 0;
+    // long sides in (max(wave_max, reg_max), lsap_mreg_max_cols] with short
+    // sides <= 1024: G = ceil(long / 4096) workgroups per problem with the
+    // column state in registers, persistent slots of G co-resident workgroups
+    int mreg_max = o.lsap_mreg_max_cols == 0 ? kMregMaxCols : o.lsap_mreg_max_cols;
+    mreg_max = mreg_max < 0 ? 0 : (mreg_max > kMregMaxCols ? kMregMaxCols : mreg_max);
+    a.mreg_lo = wave_max > a.reg_max_cols ? wave_max : a.reg_max_cols;
+    if (big && mreg_max > a.mreg_lo && overlaps((int64_t)a.mreg_lo + 1, mreg_max)) {
+        const int64_t hi = long_max < mreg_max ? long_max : mreg_max;
+        const int mg = (int)((hi + kMregCols - 1) / kMregCols);
+        const int cap = (int)(long_max < kRegMaxShort ? long_max : kRegMaxShort);
+        const size_t lds = mreg_lds_bytes(cap);
+        const void *kern = reinterpret_cast<const void *>(&lsap_mreg_kernel<CT>);
+        int occ = 0, cus = 0, dev = 0;
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, kMregNT, lds) == hipSuccess) {
+            // slots in whole groups of 8 (one per XCD): the grid never exceeds co-residency
+            const int64_t per_xcd = (int64_t)cus * occ / (8 * mg);
+            const int64_t slots = per_xcd * 8 < n_problems ? per_xcd * 8 : n_problems;
+            if (slots >= 1) {
+                a.mreg_g = mg;
+                a.mreg_slots = (int32_t)slots;
+                a.mreg_max_cols = mreg_max;
+                a.mreg_nr_cap = cap;
+                if (hipMemsetAsync(a.sync, 0, sync_bytes, s) != hipSuccess)
+                    return mvm_fail(MVM_ERR_HIP, "hipMemsetAsync(lsap sync) failed");
+                int32_t n_arg = n_problems;
+                void *params[] = {&a, &n_arg};
+                const dim3 grid((unsigned)(8 * mg * ((slots + 7) / 8))), block(kMregNT);
+                if (hipLaunchCooperativeKernel(kern, grid, block, params, (unsigned)lds, s) != hipSuccess) {
+                    (void)hipGetLastError();
+                    a.mreg_g = 0;                  // the other classes take these problems
+                }
+            }
+        }
+    }
     // Few large problems: G co-resident workgroups per problem (cooperative
     // launch guarantees co-residency).  Default: as many workgroups per
     // problem as the chip holds, up to 16, when that is at least 2; -1 off.
@@ -1262,9 +1837,6 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
     }
     // long sides in (wave_max, lsap_reg_max_cols] with short sides <= 1024:
     // one workgroup per problem with the column state in registers
-    int reg_max = o.lsap_reg_max_cols == 0 ? kRegMaxCols : o.lsap_reg_max_cols;
-    reg_max = reg_max < 0 ? 0 : (reg_max > kRegMaxCols ? kRegMaxCols : reg_max);
-    a.reg_max_cols = reg_max > wave_max ? reg_max : 0;
     if (a.multi_g <= 1 && big && a.reg_max_cols > 0 && overlaps((int64_t)wave_max + 1, a.reg_max_cols)) {
         a.reg_nc_cap = (int32_t)(long_max < a.reg_max_cols ? long_max : a.reg_max_cols);
         a.reg_nr_cap = (int32_t)(long_max < kRegMaxShort ? long_max : kRegMaxShort);
@@ -1395,7 +1967,7 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
                    ~(uintptr_t)255),   // at or after the per-problem regions (all 256-aligned)
-               0, 0, 0, 0, 0};
+               0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (cost_dtype == MVM_F64)
         return lsap_launch<double>(a, n_problems, sync_bytes, long_min, long_max, o, s);

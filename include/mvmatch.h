@@ -114,6 +114,10 @@ typedef struct mvm_options {
                                        column state in registers (ABI 3) */
     int32_t lsap_reg_threads;       /* 0 default (512 threads, 8 columns each); 1024
                                        (4 each) */
+    int32_t lsap_mreg_max_cols;     /* 0 default (65536); -1 off: long sides above
+                                       lsap_reg_max_cols up to this (short sides <= 1024)
+                                       over ceil(long / 4096) co-resident workgroups with
+                                       the column state in registers (ABI 3) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

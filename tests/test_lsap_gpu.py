@@ -24,7 +24,8 @@ def _batched(cuda, mats, options=None, dtype=np.float32):
     return [(r[o[k]:o[k + 1]], c[o[k]:o[k + 1]], int(st[k])) for k in range(len(mats))]
 
 
-@pytest.fixture(params=["default", "reg", "reg1024", "lds", "workgroup", "workgroup256", "multi"])
+@pytest.fixture(params=["default", "reg", "reg1024", "mreg", "lds", "workgroup", "workgroup256", "multi",
+                        "nomreg"])
 def lsap_path(request):
     """mvm_options of each assignment kernel class.  default: long sides <=
     1024 one problem per wave, up to 4096 (short sides <= 1024) one workgroup
@@ -34,14 +35,20 @@ def lsap_path(request):
     register-state workgroup (512 / 1024 threads); lds: every problem of <=
     4096 in the LDS-state workgroup; workgroup: one 1024-thread workgroup per
     problem with the state in the workspace; workgroup256: the same with 256
-    threads; multi: every problem split over 4 workgroups."""
-    off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1}
+    threads; multi: every problem split over 4 workgroups; mreg: every problem
+    with a short side <= 1024 in the register-state kernel spread over
+    ceil(long / 4096) workgroups (the default above 4096 columns), small
+    ones included; nomreg: the default without it (long sides above 4096 in
+    the split / LDS / workspace kernels)."""
+    off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_mreg_max_cols": -1}
     noreg = dict(off, lsap_reg_max_cols=-1)
     return {"default": None, "reg": off, "reg1024": dict(off, lsap_reg_threads=1024),
+            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1},
             "lds": noreg,
             "workgroup": dict(noreg, lsap_lds_max_cols=-1),
             "workgroup256": dict(noreg, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
-            "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4}}[request.param]
+            "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4, "lsap_mreg_max_cols": -1},
+            "nomreg": {"lsap_mreg_max_cols": -1}}[request.param]
 
 
 def test_random_shapes_and_ties_batched(cuda, lsap_path):
@@ -50,7 +57,8 @@ def test_random_shapes_and_ties_batched(cuda, lsap_path):
     for shape in [(1, 1), (3, 5), (5, 3), (7, 7), (40, 9), (9, 40), (64, 16), (300, 20), (0, 4), (4, 0),
                   (65, 2), (129, 7), (257, 30), (600, 24), (24, 600), (1024, 3), (1100, 5), (70, 70),
                   (4096, 6), (6, 4096), (2500, 11), (4097, 3), (513, 7), (768, 5), (5, 768), (769, 4),
-                  (1025, 2), (4096, 64), (1100, 1100), (1030, 1025)]:
+                  (1025, 2), (4096, 64), (1100, 1100), (1030, 1025), (5000, 20), (20, 5000),
+                  (8193, 8), (12000, 30)]:
         for trial in range(4):
             c = rng.normal(size=shape).astype(np.float32)
             if trial == 1:
@@ -143,17 +151,43 @@ def test_drop_in_error_messages(cuda):
     assert list(c) == [1, 0]
 
 
+def test_register_split_class_edges(cuda, lsap_path):
+    """Around the split register-state class: long sides 4,097 and 65,536
+    (16 workgroups) and 65,537 (beyond: another kernel), the 1,024 short side
+    at its LDS capacity, and error problems between valid ones of one slot."""
+    rng = np.random.default_rng(11)
+    mats = [rng.normal(size=(65536, 5)).astype(np.float32),
+            rng.normal(size=(3, 65537)).astype(np.float32),
+            rng.normal(size=(4500, 1024)).astype(np.float32),
+            np.round(rng.normal(size=(4097, 64)) * 2).astype(np.float32)]
+    for m, (r, c, st) in zip(mats, _batched(cuda, mats, lsap_path)):
+        r0, c0 = scipy_lsa(m)
+        assert st == 0 and np.array_equal(r, r0) and np.array_equal(c, c0), m.shape
+    nan = rng.normal(size=(5000, 4)).astype(np.float32)
+    nan[4321, 2] = np.nan
+    inf = rng.normal(size=(5000, 3)).astype(np.float32)
+    inf[:, 1] = np.inf
+    ok = rng.normal(size=(6000, 7)).astype(np.float32)
+    got = _batched(cuda, [nan, inf, ok, nan, ok], lsap_path)
+    assert [g[2] for g in got] == [1, 2, 0, 1, 0]
+    r0, c0 = scipy_lsa(ok)
+    for r, c, _ in (got[2], got[4]):
+        assert np.array_equal(r, r0) and np.array_equal(c, c0)
+
+
 @pytest.mark.parametrize("multi_g", [0, -1, 16])
 def test_full_256_cube_equals_scipy(cuda, multi_g):
     """Config-2 scale: the (65536 x 256) flattened 256^3 cube of one scene
-    (auto workgroups per problem, one, sixteen)."""
+    (default: the split register-state kernel; one workgroup; sixteen
+    workgroups of the split workspace-state kernel)."""
     from bpc_baseline_amd.synth import make_scenes
     from oracle import oracle as O
     b = make_scenes(1, 3, 256, seed=42)
     cube, _, _, _, _ = O.cube(b.pts, b.cam_offs, b.F, 1)
     flat = cube.reshape(256 * 256, 256)
     r0, c0 = scipy_lsa(flat)
-    r1, c1, st = _batched(cuda, [flat], {"lsap_multi_g": multi_g})[0]
+    opts = {"lsap_multi_g": multi_g} if multi_g == 0 else {"lsap_multi_g": multi_g, "lsap_mreg_max_cols": -1}
+    r1, c1, st = _batched(cuda, [flat], opts)[0]
     assert st == 0 and np.array_equal(r0, r1) and np.array_equal(c0, c1)
 
 

@@ -21,7 +21,9 @@ VARIANTS = {"default": {},
             "lds1024": dict(OFF, lsap_lds_small_cols=-1),
             "lds256": dict(OFF, lsap_lds_small_cols=4096),
             "wg256": dict(OFF, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
-            "wg1024": dict(OFF, lsap_lds_max_cols=-1, lsap_mid_max_cols=-1)}
+            "wg1024": dict(OFF, lsap_lds_max_cols=-1, lsap_mid_max_cols=-1),
+            "nomreg": {"lsap_mreg_max_cols": -1},
+            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1}}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=1000)
