@@ -1369,10 +1369,13 @@ __device__ __forceinline__ int transpose_rows(const CT *C0, CT *Ctw, int r_lo, i
                                               int64_t ld_out, CT (*s_tile)[kTile * 4 / sizeof(CT) + 1]) {
     constexpr int kT = kTile * 4 / (int)sizeof(CT), E = kT * kT / NT;
     static_assert(E * NT == kT * kT, "a tile is E elements per thread");
-    const int t = threadIdx.x;
     const int ntc = (ncols + kT - 1) / kT, ntiles = (r_hi - r_lo + kT - 1) / kT * ntc;
     int bad = 0;
     for (int tb = 0; tb < ntiles; tb += D) {
+        // the per-element tile coordinates are recomputed per group (cheap), not
+        // hoisted out of the caller's problem loop into spilled registers
+        int t = threadIdx.x;
+        asm volatile("" : "+v"(t));
         CT val[D][E];
 #pragma unroll
         for (int d = 0; d < D; ++d) {                        // all D tiles' loads first
@@ -1503,6 +1506,18 @@ __global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32
 
         // ---- one shortest augmenting path per short-side row -------------
         MREG_PT(0);                                          // validate + transpose + first exchange
+        // the next cost row's loads are issued as soon as the row is known: after
+        // a step's decision, and for the next search's first row before this
+        // search's end work (duals, walk, barrier), which then hides their latency
+        CT cq[K];
+        auto load_row = [&](int row) {
+            const CT *Ci = Ct + (int64_t)row * nc + c0;
+            int lim = __builtin_amdgcn_readfirstlane(own > 0 ? own - 1 : 0);   // c0 < nc
+            asm volatile("" : "+s"(lim));
+#pragma unroll
+            for (int q = 0; q < K; ++q) cq[q] = Ci[min(t + NT * q, lim)];
+        };
+        if (nr > 0) load_row(0);
         for (int cur = 0; cur < nr; ++cur) {
             uint32_t insc = 0;
             // per-search and per-step uniforms are laundered through an SGPR so
@@ -1518,15 +1533,9 @@ __global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32
             }
             int i = cur, nrem = nc, k = 0, sink = -1;
             double min_val = 0.0;
-            __syncthreads();                                 // the previous row's replay is in place
+            // (the previous row's replay is in place: the barrier after the walk)
             while (true) {
                 const double ui = s_u[i];
-                const CT *Ci = Ct + (int64_t)i * nc + c0;
-                int lim = __builtin_amdgcn_readfirstlane(own > 0 ? own - 1 : 0);   // c0 < nc
-                asm volatile("" : "+s"(lim));
-                CT cq[K];
-#pragma unroll
-                for (int q = 0; q < K; ++q) cq[q] = Ci[min(t + NT * q, lim)];   // all loads first
                 URed best{INFINITY, ~0u, 0u};
 #pragma unroll
                 for (int q = 0; q < K; ++q) {
@@ -1632,6 +1641,7 @@ __global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32
                     break;
                 }
                 i = r4;
+                load_row(i);
                 MREG_PT(5);                                  // combine + decision
                 if (++k > nr) {                              // a step list overflow cannot happen
                     if (t == 0) atomicExch(&sb->flag, 3);
@@ -1639,9 +1649,13 @@ __global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32
                 }
             }
             if (sink < 0) break;                             // infeasible
+            if (cur + 1 < nr) load_row(cur + 1);
 #pragma unroll
-            for (int q = 0; q < K; ++q)
+            for (int q = 0; q < K; ++q) {
                 if ((insc >> q) & 1u) v[q] -= min_val - spc[q];
+                // the only free column a search visits is its sink, now assigned
+                if (c0 + t + NT * q == sink) freem &= ~(1u << q);
+            }
             // row duals: u[cur] += minVal; u[i_k] += minVal - spc[col4row[i_k]]
             // with col4row[i_k] = j_(k-1), whose spc is step k-1's minimum (rows
             // distinct: one lane each)
@@ -1660,9 +1674,6 @@ __global__ __launch_bounds__(kMregNT, 4) void lsap_mreg_kernel(LsapArgs a, int32
                 }
             }
             __syncthreads();
-#pragma unroll
-            for (int q = 0; q < K; ++q)                      // path columns (all visited) now have rows
-                if ((insc >> q) & 1u) freem &= s_r4c[t + NT * q] == -1 ? ~0u : ~(1u << q);
             MREG_PT(6);                                      // search end: duals, walk
         }
         __syncthreads();
