@@ -48,8 +48,9 @@ struct PairArgs {
     int32_t n_cams, n_pairs, row_blocks;
     int32_t rows_per_wg;        // kWaves * RPW * row groups
     int32_t col_tile;           // columns whose lines are resident in LDS (multiple of kChunk)
-    int32_t lazy;               // clean row groups: 1 lazy argmin + transposed reduction,
-                                // 0 eager (mvm_options)
+    int32_t lazy;               // 1: association by pairwise_lazy_kernel when the view fits
+                                // one column tile; 0: eager argmin (mvm_options)
+    int32_t row_slots;          // lazy kernel: row-line slots per wave in LDS
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -249,163 +250,181 @@ __device__ __forceinline__ void lazy_reduce_bits(uint32_t *red, const uint32_t (
 }
 
 
-// Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair).  The
-// normalised lines of (up to col_tile) columns are computed ONCE per
-// workgroup into LDS; each wave then sweeps groups of RPW rows: per 256-column
-// chunk every lane holds 4 consecutive columns in registers and walks the
-// RPW rows, one coalesced 16-byte store per lane per row.
-// occupancy OCC: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below
-// (RPW 16 at 4 waves/SIMD spills and measured slower: DESIGN.md §3.1); 2 when
-// the workgroup's LDS allows no more anyway (the host picks it)
-template <int RPW, bool ARGMIN, typename OutT, int NT = 1, int OCC = (RPW >= 16 ? 3 : 4)>
-__global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
-    const int T = args.col_tile;
-    double *s_l0 = reinterpret_cast<double *>(s_dyn);
-    double *s_l1 = s_l0 + T;
-    double *s_l2 = s_l1 + T;
-    double *s_x = s_l2 + T;
-    double *s_y = s_x + T;
-    // per wave: the row lines of up to 64 rows (all its groups when they fit)
-    double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
-    double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
-    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
-    // lazy argmin: per wave an [RPW][64] u32 scratch for the transposed reduction
-    uint32_t *s_red = s_cst + T;
+// ---- workgroup set-up shared by both kernels ----
+// The workgroup's (scene, pair, row block) and the geometry of its matrix.
+struct BlockGeom {
+    int sp, na, nb, row0;
+    int64_t oa, ob;
+    int64_t doff;       // first float of the matrix in `dist`
+    int64_t row_off0;   // first association row of the matrix
+    int64_t ld;         // row stride (pitch)
+    int lim;            // columns a row stores: its padding too when pitched
+};
 
-    const int t = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
-    const int lane = t % kWave;
-    // dispatch places workgroup b on XCD b % 8; each XCD walks a contiguous
-    // range of (scene, pair, row block)s, so a (scene, pair)'s row blocks
-    // share one L2 and its output region stays contiguous per XCD
+// Dispatch places workgroup b on XCD b % 8; the remap lets each XCD walk a
+// contiguous range of (scene, pair, row block)s, so a (scene, pair)'s row
+// blocks share one L2 for the column points and its output region stays
+// contiguous per XCD.  Every global load here comes before the first store
+// (on CDNA vmcnt orders loads behind earlier stores).  Returns false when the
+// block lies past its matrix's rows (uniform over the workgroup).
+__device__ __forceinline__ bool block_geometry(const PairArgs &args, double (&f)[9], BlockGeom &g) {
     uint32_t blk = blockIdx.x;
     {
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
         blk = x * q + min(x, r) + blk / 8;
     }
     const int rb = (int)(blk % (uint32_t)args.row_blocks);
-    const int sp = (int)(blk / (uint32_t)args.row_blocks);
-    const int s = sp / args.n_pairs;
-    const int p = sp - s * args.n_pairs;
+    g.sp = (int)(blk / (uint32_t)args.row_blocks);
+    const int s = g.sp / args.n_pairs;
+    const int p = g.sp - s * args.n_pairs;
     const int cam_a = args.pair_a[p], cam_b = args.pair_b[p];
-    const int64_t oa = args.cam_offs[(int64_t)s * args.n_cams + cam_a];
-    const int na = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_a + 1] - oa);
-    const int64_t ob = args.cam_offs[(int64_t)s * args.n_cams + cam_b];
-    const int nb = (int)(args.cam_offs[(int64_t)s * args.n_cams + cam_b + 1] - ob);
-    // rows of the workgroup: [row0, row0 + rows_per_wg)
-    constexpr int U = kWaves * RPW;
-    const int row0 = rb * args.rows_per_wg;
-    if (row0 >= na) return;   // uniform over the workgroup
-
-    double f[9];
+    const int64_t *co = args.cam_offs + (int64_t)s * args.n_cams;
+    g.oa = co[cam_a];
+    g.na = (int)(co[cam_a + 1] - g.oa);
+    g.ob = co[cam_b];
+    g.nb = (int)(co[cam_b + 1] - g.ob);
+    g.row0 = rb * args.rows_per_wg;
+    if (g.row0 >= g.na) return false;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) f[k] = args.F[(int64_t)sp * 9 + k];
-
-    const int64_t doff = args.dist_offs ? args.dist_offs[sp] : (int64_t)sp * args.mat_stride;
-    // first association row of this matrix, loaded before any store (a vector
-    // load issued after the stores would wait for all of them: vmcnt is in order)
-    const int64_t row_off0 = args.row_offs ? args.row_offs[sp] : 0;
+    for (int k = 0; k < 9; ++k) f[k] = args.F[(int64_t)g.sp * 9 + k];
+    g.doff = args.dist_offs ? args.dist_offs[g.sp] : (int64_t)g.sp * args.mat_stride;
+    g.row_off0 = args.row_offs ? args.row_offs[g.sp] : 0;
     const int ra = args.row_align > 1 ? args.row_align : 1;
-    const int64_t ld = args.ld ? args.ld : (int64_t)((nb + ra - 1) / ra) * ra;
-    // columns a row stores: its padding too when pitched, so whole lines go out
-    const int lim = (int)min(ld, (int64_t)0x7FFFFFFF);
-    OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + doff : nullptr;
-    const bool vec_ok = dbase && ((doff & 3) == 0) && ((ld & 3) == 0);
-    // unaligned float32 rows: lanes take strided columns (coalesced dword stores)
-    const bool strided = dbase && !vec_ok && sizeof(OutT) == 4;
+    g.ld = args.ld ? args.ld : (int64_t)((g.nb + ra - 1) / ra) * ra;
+    g.lim = (int)min(g.ld, (int64_t)0x7FFFFFFF);
+    return true;
+}
 
-    // column lines of columns [c0, c0 + T) -> LDS (threads stride the tile)
-    auto load_tile = [&](int c0) {
-        for (int jj = t; jj < T; jj += kThreads) {
-            const int j = c0 + jj;
-            // past the view: a pad line, whose pair values are +inf (l1.p1 = +inf,
-            // l2.p2 = rl2 finite) -- never a row minimum, and what a pitched
-            // row's padding holds
-            uint32_t st = kNone;
-            double l0 = 0, l1 = 0, l2 = __builtin_inf(), x = 0, y = 0;
-            if (j < nb) {
-                x = args.pts[2 * (ob + j)];
-                y = args.pts[2 * (ob + j) + 1];
-                st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
-            }
-            s_l0[jj] = l0;
-            s_l1[jj] = l1;
-            s_l2[jj] = l2;
-            s_x[jj] = x;
-            s_y[jj] = y;
-            s_cst[jj] = st;
+// Column lines of columns [c0, c0 + T) of the view -> LDS (threads stride the
+// tile).  Past the view: a pad line, whose pair values are +inf (l1.p1 =
+// +inf, l2.p2 = rl2 finite) -- never a row minimum, and what a pitched row's
+// padding holds.
+__device__ __forceinline__ void load_col_lines(const double *pts, const double (&f)[9], int64_t ob,
+                                               int nb, int c0, int T, double *s_l0, double *s_l1,
+                                               double *s_l2, double *s_x, double *s_y,
+                                               uint32_t *s_cst) {
+    for (int jj = threadIdx.x; jj < T; jj += kThreads) {
+        const int j = c0 + jj;
+        uint32_t st = kNone;
+        double l0 = 0, l1 = 0, l2 = __builtin_inf(), x = 0, y = 0;
+        if (j < nb) {
+            x = pts[2 * (ob + j)];
+            y = pts[2 * (ob + j) + 1];
+            st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
         }
-    };
-    // every global load of the workgroup's rows happens here, before the first
-    // store (on CDNA vmcnt orders loads behind earlier stores)
-    for (int x = t; x < args.rows_per_wg; x += kThreads) {
+        s_l0[jj] = l0;
+        s_l1[jj] = l1;
+        s_l2[jj] = l2;
+        s_x[jj] = x;
+        s_y[jj] = y;
+        s_cst[jj] = st;
+    }
+}
+
+// Row centroids of the workgroup's rows [row0, row0 + rows) -> LDS.
+__device__ __forceinline__ void load_row_points(const double *pts, int64_t oa, int na, int row0,
+                                                int rows, double *s_rpt) {
+    for (int x = threadIdx.x; x < rows; x += kThreads) {
         const int i = row0 + x;
-        const f64x2 v = (i < na) ? *reinterpret_cast<const f64x2 *>(args.pts + 2 * (oa + i))
+        const f64x2 v = (i < na) ? *reinterpret_cast<const f64x2 *>(pts + 2 * (oa + i))
                                  : f64x2{0.0, 0.0};
         *reinterpret_cast<f64x2 *>(s_rpt + 2 * x) = v;
     }
-    const int n_tiles = (nb + T - 1) / T;
-    if (n_tiles == 1) load_tile(0);
-    // lazy argmin needs every column of the (single) tile clean
-    // (padding columns are pad lines: clean for the lazy argmin)
-    bool my_clean = n_tiles == 1 && nb > 0;
-    if (ARGMIN && sizeof(OutT) == 4 && args.lazy && n_tiles == 1)
-        for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] != kDeg && s_cst[jj] != kWild);
+}
+
+// Line {l0, l1, l2, x, y, state} of local row xw + row into `slot` (6 doubles);
+// rows past the view (row >= nrows) get a degenerate record.
+__device__ __forceinline__ void put_row_line(double *slot, const double *s_rpt,
+                                             const double (&f)[9], int xw, int row, int nrows) {
+    double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
+    bool deg = true;
+    if (row < nrows) {
+        x = s_rpt[2 * (xw + row)];
+        y = s_rpt[2 * (xw + row) + 1];
+        deg = row_line(f, x, y, l0, l1, l2);
+    }
+    slot[0] = l0;
+    slot[1] = l1;
+    slot[2] = l2;
+    slot[3] = x;
+    slot[4] = y;
+    slot[5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
+}
+
+// ---- the default association kernel (lazy argmin) ----
+// Workgroup = 4 waves owning rows_per_wg rows of one (scene, pair) whose view
+// fits one column tile (<= kMaxColTile columns).  The column lines are
+// computed ONCE per workgroup into LDS; each wave sweeps groups of RPW rows:
+// per 256-column chunk every lane holds 4 consecutive columns in registers
+// and walks the RPW rows, one coalesced 16-byte store per lane per row, and
+// keeps per row only the float32 bits of its minimum (lazy argmin, resolved
+// at the group end).  A row group with a degenerate or non-finite line, or a
+// matrix whose rows are not 16-byte aligned, runs the generic arithmetic one
+// row at a time instead (rare; correctness only).  The eager, strided and
+// multi-tile forms live in pairwise_kernel: kept out of this kernel, they
+// cannot raise its register allocation or hoist their uniforms into
+// SGPR spills around the lazy loop.
+// Occupancy OCC: 3 waves/SIMD at RPW 16, 4 below; 2 when the workgroup's LDS
+// allows no more anyway (the host picks it).
+template <int RPW, int NT, int OCC = (RPW >= 16 ? 3 : 4)>
+__global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int T = args.col_tile;
+    const int RS = args.row_slots;   // row-line slots per wave
+    double *s_l0 = reinterpret_cast<double *>(s_dyn);
+    double *s_l1 = s_l0 + T;
+    double *s_l2 = s_l1 + T;
+    double *s_x = s_l2 + T;
+    double *s_y = s_x + T;
+    double *s_rows = s_y + T;                          // [kWaves][RS][6]
+    double *s_rpt = s_rows + kWaves * RS * 6;          // row centroids of the workgroup
+    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
+    uint32_t *s_red = s_cst + T;                       // per wave an [RPW][64] u32 scratch
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
+    const int lane = t % kWave;
+    double f[9];
+    BlockGeom g;
+    if (!block_geometry(args, f, g)) return;
+    const int na = g.na, nb = g.nb, row0 = g.row0;
+    float *const dbase = args.dist ? reinterpret_cast<float *>(args.dist) + g.doff : nullptr;
+    const bool vec_ok = dbase && ((g.doff & 3) == 0) && ((g.ld & 3) == 0);
+    constexpr int U = kWaves * RPW;
+
+    load_row_points(args.pts, g.oa, na, row0, args.rows_per_wg, s_rpt);
+    load_col_lines(args.pts, f, g.ob, nb, 0, T, s_l0, s_l1, s_l2, s_x, s_y, s_cst);
+    // the lazy argmin needs every column of the tile clean (pad lines count as clean)
+    bool my_clean = nb > 0;
+    for (int jj = t; jj < T; jj += kThreads) my_clean &= (s_cst[jj] != kDeg && s_cst[jj] != kWild);
     const bool tile_clean = __syncthreads_and(my_clean) != 0;
 
     const int n_groups = (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
-    // group g's geometry: first local row, matrix row, rows
-    auto group_rows = [&](int g, int &xw, int &grow0, int &nrows) {
-        xw = (g * kWaves + wave) * RPW;
-        grow0 = row0 + xw;
-        nrows = min(RPW, na - grow0);                          // may be <= 0
-    };
-    // line of local row xw + row into slot `slot` of the wave's LDS rows
-    auto put_row_line = [&](int slot, int xw, int row, int nrows) {
-        double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
-        bool deg = true;
-        if (row < nrows) {
-            x = s_rpt[2 * (xw + row)];
-            y = s_rpt[2 * (xw + row) + 1];
-            deg = row_line(f, x, y, l0, l1, l2);
-        }
-        s_row[wave][slot][0] = l0;
-        s_row[wave][slot][1] = l1;
-        s_row[wave][slot][2] = l2;
-        s_row[wave][slot][3] = x;
-        s_row[wave][slot][4] = y;
-        s_row[wave][slot][5] = (double)(deg ? kDeg : (tame(l2, x, y) ? kOk : kWild));
-    };
-    // all of the wave's groups fit in 64 rows: one lane per row computes every
-    // row line up front (one pass instead of one 16-lane pass per group)
-    const bool pre = RPW * n_groups <= kWave;   // uniform
+    double *const s_roww = s_rows + wave * RS * 6;
+    // all of the wave's groups fit its row slots: one lane per row computes
+    // every row line up front (one pass instead of one 16-lane pass per group)
+    const bool pre = RPW * n_groups <= RS;   // uniform
     if (pre && lane < RPW * n_groups) {
-        int xw, grow0, nrows;
-        const int g = lane / RPW, slot = lane % RPW;
-        group_rows(g, xw, grow0, nrows);
-        put_row_line(lane, xw, slot, nrows);
+        const int gi = lane / RPW, slot = lane % RPW;
+        const int xw = (gi * kWaves + wave) * RPW;
+        put_row_line(s_roww + 6 * lane, s_rpt, f, xw, slot, min(RPW, na - (row0 + xw)));
     }
-    for (int g = 0; g < n_groups; ++g) {
-        int xw, grow0, nrows;
-        group_rows(g, xw, grow0, nrows);
-        double(*rowp)[6] = s_row[wave] + (pre ? g * RPW : 0);   // this group's slots
+    for (int gi = 0; gi < n_groups; ++gi) {
+        const int xw = (gi * kWaves + wave) * RPW;
+        const int grow0 = row0 + xw;
+        const int nrows = min(RPW, na - grow0);                 // may be <= 0
+        double(*rowp)[6] = reinterpret_cast<double(*)[6]>(s_roww + (pre ? gi * RPW * 6 : 0));
         if (!pre && lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
             int lz = lane;          // fresh per group: its LDS address is not hoisted and spilled
             __asm__ volatile("" : "+v"(lz));
-            put_row_line(lz, xw, lz, nrows);
+            put_row_line(s_roww + 6 * lz, s_rpt, f, xw, lz, nrows);
         }
+        if (nrows <= 0) continue;
         // the same wave reads them back (LDS executes one wave's ops in order)
         const bool rows_fast =
             (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
-
-        Best best[RPW];
-#pragma unroll
-        for (int r = 0; r < RPW; ++r) best[r] = Best{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
         // uniform: the whole group takes the lazy argmin (clean rows and tile)
-        const bool lazy = ARGMIN && sizeof(OutT) == 4 && args.lazy && args.row_offs &&
-                          tile_clean && rows_fast && (vec_ok || !dbase);
-        if (lazy) {
+        if (tile_clean && rows_fast && (vec_ok || !dbase)) {
             uint32_t bbits[RPW];
 #pragma unroll
             for (int r = 0; r < RPW; ++r) bbits[r] = 0x7F800000u;
@@ -413,7 +432,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                 const int jbase = c0 + kColsPerLane * lane;
                 // the last chunk of a ragged view: lanes past the row's pitch
                 // sit out (their columns hold pad lines: +inf, never a minimum)
-                if (jbase >= lim) continue;
+                if (jbase >= g.lim) continue;
                 ColRegs c;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
@@ -425,8 +444,30 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                     c.y[q] = s_y[jj];
                 }
                 if (dbase) {
-                    const uint64_t rstep = (uint64_t)ld * sizeof(OutT);
-                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * ld);
+                    const uint64_t rstep = (uint64_t)g.ld * sizeof(float);
+                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * g.ld);
+#ifdef MVM_ROW_PREFETCH
+                    // row r + 1's line is read from LDS before row r is
+                    // computed (the scheduling barrier keeps the reads there),
+                    // so its LDS latency hides behind row r's arithmetic
+                    double cur[5], nxt[5];
+#pragma unroll
+                    for (int e = 0; e < 5; ++e) cur[e] = rowp[0][e];
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        if (r + 1 < RPW) {
+#pragma unroll
+                            for (int e = 0; e < 5; ++e) nxt[e] = rowp[r + 1][e];
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                        row_fast_lazy<true, NT>(c, cur[0], cur[1], cur[2], cur[3], cur[4],
+                                                reinterpret_cast<float *>(rp), jbase, bbits[r]);
+                        rp += rstep;
+                        __asm__ volatile("" : "+s"(rp));
+#pragma unroll
+                        for (int e = 0; e < 5; ++e) cur[e] = nxt[e];
+                    }
+#else
 #pragma unroll
                     for (int r = 0; r < RPW; ++r) {
                         row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1], rowp[r][2],
@@ -438,6 +479,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                         // (they would be spilled to VGPR lanes)
                         __asm__ volatile("" : "+s"(rp));
                     }
+#endif
                 } else {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r)
@@ -463,15 +505,14 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
             bool tie;
             lazy_reduce_bits<RPW>(s_red + wave * (RPW * kWave), bbits, lz, k, w, tie);
             // the LPR lanes of row slot rs recompute lane w's values in
-            // every chunk (slot idx = chunk * 4 + q; lazy tiles have
-            // nb == T, a multiple of kChunk) and keep the first equal to k
+            // every chunk (slot idx = chunk * 4 + q) and keep the first equal to k
             const int rs = lz / LPR, seg = lz % LPR;
             const int n_ch = (nb + kChunk - 1) / kChunk;
             const double *rl = rowp[rs];
             uint32_t first = 0xFFFFFFFFu;
 #pragma unroll
-            for (int t = VPL - 1; t >= 0; --t) {
-                const int idx = seg + LPR * t;
+            for (int v = VPL - 1; v >= 0; --v) {
+                const int idx = seg + LPR * v;
                 const int c = idx / kColsPerLane, q = idx % kColsPerLane;
                 if (c < n_ch) {
                     const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
@@ -495,17 +536,124 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
                 }
             }
             if (seg == 0) {
-                const int64_t row = row_off0 + grow0 + rs;
+                const int64_t row = g.row_off0 + grow0 + rs;
                 if (args.argmin) args.argmin[row] = jwin;
                 if (args.minval) args.minval[row] = __uint_as_float(k);
             }
             continue;
         }
+        // generic rows, one at a time: degenerate lines (9999 sentinel),
+        // non-finite or huge values, rows off 16-byte alignment (lanes then
+        // take strided columns: each dword store instruction writes 256
+        // contiguous bytes)
+        const bool str = dbase && !vec_ok;
+        for (int r = 0; r < nrows; ++r) {
+            const double *rl = rowp[r];
+            const bool rdeg = __builtin_amdgcn_readfirstlane((int)rl[5]) == (int)kDeg;
+            float *drow = dbase ? dbase + (int64_t)(grow0 + r) * g.ld : nullptr;
+            Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
+            for (int c0 = 0; c0 < nb; c0 += kChunk) {
+                ColRegs c;
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    const int jj = str ? c0 + lane + kWave * q : c0 + kColsPerLane * lane + q;
+                    c.l0[q] = s_l0[jj];
+                    c.l1[q] = s_l1[jj];
+                    c.l2[q] = s_l2[jj];
+                    c.x[q] = s_x[jj];
+                    c.y[q] = s_y[jj];
+                    c.state[q] = s_cst[jj];
+                }
+                row_safe<true, float>(c, rl[0], rl[1], rl[2], rl[3], rl[4], rdeg, drow,
+                                      c0 + (str ? lane : kColsPerLane * lane), str ? kWave : 1, b,
+                                      g.lim);
+            }
+            uint32_t kmin;
+            int32_t imin;
+            wave_argmin(best_key(b), b.j, kmin, imin);
+            if (lane == 0) {
+                const int64_t row = g.row_off0 + grow0 + r;
+                if (args.argmin) args.argmin[row] = (kmin == kKeyInvalid) ? -1 : imin;
+                if (args.minval) args.minval[row] = value_of_key(kmin);
+            }
+        }
+    }
+}
 
+// ---- the general kernel ----
+// Everything the lazy kernel does not take: matrices without association
+// (ARGMIN false), float64 output (the cube's workspace, epipolar_error),
+// the eager argmin (MVM_PAIRWISE_ARGMIN_EAGER) and views of more than
+// kMaxColTile columns (column lines streamed tile by tile).  Same workgroup
+// layout; per row group an eager argmin (float best + index per row in
+// registers) reduced across the wave at the group end.
+// occupancy OCC: 3 waves/SIMD (<= 168 VGPRs) at RPW 16, 4 (<= 128) below; 2
+// when the workgroup's LDS allows no more anyway (the host picks it)
+template <int RPW, bool ARGMIN, typename OutT, int NT = 1, int OCC = (RPW >= 16 ? 3 : 4)>
+__global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int T = args.col_tile;
+    double *s_l0 = reinterpret_cast<double *>(s_dyn);
+    double *s_l1 = s_l0 + T;
+    double *s_l2 = s_l1 + T;
+    double *s_x = s_l2 + T;
+    double *s_y = s_x + T;
+    // per wave: the row lines of up to 64 rows (all its groups when they fit)
+    double(*s_row)[kWave][6] = reinterpret_cast<double(*)[kWave][6]>(s_y + T);
+    double *s_rpt = s_y + T + kWaves * kWave * 6;            // row centroids of the workgroup
+    uint32_t *s_cst = reinterpret_cast<uint32_t *>(s_rpt + 2 * args.rows_per_wg);
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);   // uniform by construction
+    const int lane = t % kWave;
+    double f[9];
+    BlockGeom g;
+    if (!block_geometry(args, f, g)) return;
+    const int na = g.na, nb = g.nb, row0 = g.row0;
+    const int64_t ld = g.ld;
+    const int lim = g.lim;
+    constexpr int U = kWaves * RPW;
+    OutT *const dbase = args.dist ? reinterpret_cast<OutT *>(args.dist) + g.doff : nullptr;
+    const bool vec_ok = dbase && ((g.doff & 3) == 0) && ((ld & 3) == 0);
+    // unaligned float32 rows: lanes take strided columns (coalesced dword stores)
+    const bool strided = dbase && !vec_ok && sizeof(OutT) == 4;
+
+    load_row_points(args.pts, g.oa, na, row0, args.rows_per_wg, s_rpt);
+    const int n_tiles = (nb + T - 1) / T;
+    if (n_tiles == 1) load_col_lines(args.pts, f, g.ob, nb, 0, T, s_l0, s_l1, s_l2, s_x, s_y, s_cst);
+    __syncthreads();
+
+    const int n_groups = (min(args.rows_per_wg, na - row0) + U - 1) / U;   // uniform over the WG
+    // all of the wave's groups fit in 64 rows: one lane per row computes every
+    // row line up front (one pass instead of one 16-lane pass per group)
+    const bool pre = RPW * n_groups <= kWave;   // uniform
+    if (pre && lane < RPW * n_groups) {
+        const int gi = lane / RPW, slot = lane % RPW;
+        const int xw = (gi * kWaves + wave) * RPW;
+        put_row_line(s_row[wave][lane], s_rpt, f, xw, slot, min(RPW, na - (row0 + xw)));
+    }
+    for (int gi = 0; gi < n_groups; ++gi) {
+        const int xw = (gi * kWaves + wave) * RPW;
+        const int grow0 = row0 + xw;
+        const int nrows = min(RPW, na - grow0);                 // may be <= 0
+        double(*rowp)[6] = s_row[wave] + (pre ? gi * RPW : 0);   // this group's slots
+        if (!pre && lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
+            int lz = lane;          // fresh per group: its LDS address is not hoisted and spilled
+            __asm__ volatile("" : "+v"(lz));
+            put_row_line(s_row[wave][lz], s_rpt, f, xw, lz, nrows);
+        }
+        // the same wave reads them back (LDS executes one wave's ops in order)
+        const bool rows_fast =
+            (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
+
+        Best best[RPW];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) best[r] = Best{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
         for (int tile = 0; tile < n_tiles; ++tile) {
             if (n_tiles > 1) {   // large views: stream the column lines tile by tile
                 __syncthreads();
-                load_tile(tile * T);
+                load_col_lines(args.pts, f, g.ob, nb, tile * T, T, s_l0, s_l1, s_l2, s_x, s_y,
+                               s_cst);
                 __syncthreads();
             }
             const int tile_cols = min(T, nb - tile * T);
@@ -602,7 +750,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
             int lz = lane;   // fresh per group: no hoisted, spilled row addresses
             __asm__ volatile("" : "+v"(lz));
             store_row_results<RPW>(kmin, imin, nrows, lz, args.argmin, args.minval,
-                                   row_off0 + grow0);
+                                   g.row_off0 + grow0);
         }
     }
 }
@@ -632,11 +780,15 @@ int fill_pairs(PairArgs &a, const int32_t *pair_a, const int32_t *pair_b, int n_
     return MVM_OK;
 }
 
+// LDS of a workgroup: column lines (5 doubles + a state word per column),
+// `row_slots` row lines per wave (6 doubles each), the row centroids, and for
+// the lazy kernel its per-wave [RPW][64] reduction scratch.
 template <int RPW>
-size_t pairwise_lds_bytes(int col_tile, int rows_per_wg, bool transposed_reduction) {
+size_t pairwise_lds_bytes(int col_tile, int rows_per_wg, int row_slots, bool lazy) {
     return (size_t)col_tile * (5 * sizeof(double) + sizeof(uint32_t)) +
-           (size_t)kWaves * kWave * 6 * sizeof(double) + (size_t)rows_per_wg * 2 * sizeof(double) +
-           (transposed_reduction ? (size_t)kWaves * RPW * kWave * sizeof(uint32_t) : 0);
+           (size_t)kWaves * row_slots * 6 * sizeof(double) +
+           (size_t)rows_per_wg * 2 * sizeof(double) +
+           (lazy ? (size_t)kWaves * RPW * kWave * sizeof(uint32_t) : 0);
 }
 
 // Launch with `lds` bytes of dynamic LDS (above 64 KiB the kernel must opt in).
@@ -658,20 +810,33 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
-    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, argmin && !f64 && a.lazy);
-    if (f64) return launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
     // nontemporal stores for whole-line rows (views of a multiple of 32, or
     // rows pitched to 128-byte lines); rows that end mid-line share that line
     // with the next row, and L2 must merge it (default policy)
-    if (max_cols % 32 == 0 || a.row_align % 32 == 0) {
-        // LDS allows at most two workgroups per CU (> 160 KiB / 3; C3's 1,024
-        // column lines): the register cap of three waves per SIMD buys nothing
-        // there, and at 168 VGPRs the kernel spills -- a scratch reload ahead
-        // of the lazy chunk loop makes the compiler drain every outstanding
-        // store (s_waitcnt vmcnt(0)) at each chunk.  At two waves per SIMD it
-        // has 200 VGPRs, no spills and no drain: C3 4.21 -> 4.14 ms per launch
-        // on the same four output buffers, build order rotated
-        // (tools/ab_same_buffers.py, profiles/r02/alloc/c3_occ2_same_buffers.log)
+    const bool nt = max_cols % 32 == 0 || a.row_align % 32 == 0;
+    // The default association path: the lazy kernel, for views of one column
+    // tile.  Row slots: all of a wave's row groups when they fit in 64 (one
+    // up-front row-line pass), else one group's.
+    if (argmin && !f64 && a.lazy && max_cols <= kMaxColTile) {
+        a.row_slots = RPW * row_groups <= kWave ? RPW * row_groups : RPW;
+        const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, a.row_slots, true);
+        // LDS for at most two workgroups per CU (C3's 1,024 column lines): the
+        // register cap of three waves per SIMD buys nothing there
+        const bool occ2 = lds > kLds3PerCU;
+        if (nt)
+            return occ2 ? launch_lds(pairwise_lazy_kernel<RPW, 1, 2>, grid, block, lds, stream, a)
+                        : launch_lds(pairwise_lazy_kernel<RPW, 1>, grid, block, lds, stream, a);
+        return occ2 ? launch_lds(pairwise_lazy_kernel<RPW, 0, 2>, grid, block, lds, stream, a)
+                    : launch_lds(pairwise_lazy_kernel<RPW, 0>, grid, block, lds, stream, a);
+    }
+    a.row_slots = kWave;
+    const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, kWave, false);
+    if (f64) return launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
+    if (nt) {
+        // two workgroups per CU by LDS: at 168 VGPRs (the three-waves cap) the
+        // kernel spilled, and a scratch reload ahead of a chunk loop drains
+        // every outstanding store (s_waitcnt vmcnt(0)); at two waves per SIMD
+        // it has the registers (profiles/r02/alloc/c3_occ2_same_buffers.log)
         if (argmin && lds > kLds3PerCU)
             return launch_lds(pairwise_kernel<RPW, true, float, 1, 2>, grid, block, lds, stream, a);
         if (argmin) return launch_lds(pairwise_kernel<RPW, true, float, 1>, grid, block, lds, stream, a);
@@ -727,7 +892,7 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     case 8: st = launch_pairwise_rpw<8>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
     default: st = launch_pairwise_rpw<16>(a, sp_count, max_rows, max_cols, rg, argmin, f64, stream); break;
     }
-    return st ? st : mvm_check_launch("pairwise_kernel");
+    return st ? st : mvm_check_launch("pairwise kernel");
 }
 
 }  // namespace

@@ -93,8 +93,9 @@ libs = {}
 for path in args.libs.split(","):
     lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
     for name, (res, argt) in _native.SIGNATURES.items():
-        fn = getattr(lib, name)
-        fn.restype, fn.argtypes = res, argt
+        fn = getattr(lib, name, None)   # older builds lack newer entry points
+        if fn is not None:
+            fn.restype, fn.argtypes = res, argt
     libs[os.path.basename(path)] = lib
 
 dev = torch.device("cuda", 0)
