@@ -163,13 +163,15 @@ __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double 
 // Lazy argmin: per row a lane keeps only the float32 bits of its minimum over
 // the chunks it has seen -- two v_min3_u32 per 4 pairs; the column is
 // recovered at the end of the row group (lazy_reduce_bits + recovery below)
-template <bool STORE, int NT>
+// MASKED: the last chunk of a ragged view, where lanes past the row's pitch
+// (st false) compute pad-line values (+inf, never a minimum) but store nothing.
+template <bool STORE, int NT, bool MASKED = false>
 __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
                                               double rx, double ry, float *drow, int jbase,
-                                              uint32_t &bbits) {
+                                              uint32_t &bbits, bool st = true) {
     float v[kColsPerLane];
     pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
-    if (STORE) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
+    if (STORE && (!MASKED || st)) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
     bbits = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2])),
                      __float_as_uint(v[3]), bbits);
 }
@@ -428,11 +430,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             uint32_t bbits[RPW];
 #pragma unroll
             for (int r = 0; r < RPW; ++r) bbits[r] = 0x7F800000u;
-            for (int c0 = 0; c0 < nb; c0 += kChunk) {
+            // one 256-column chunk: every lane's 4 columns x the group's rows
+            auto sweep_chunk = [&](int c0, auto masked) __attribute__((always_inline)) {
+                constexpr bool M = decltype(masked)::value;
                 const int jbase = c0 + kColsPerLane * lane;
-                // the last chunk of a ragged view: lanes past the row's pitch
-                // sit out (their columns hold pad lines: +inf, never a minimum)
-                if (jbase >= g.lim) continue;
+                const bool st = jbase < g.lim;
                 ColRegs c;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
@@ -443,13 +445,23 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                     c.x[q] = s_x[jj];
                     c.y[q] = s_y[jj];
                 }
-                if (dbase) {
+                if (dbase && M) {
+                    // the last chunk of a ragged view: lanes past the row's
+                    // pitch store nothing (per-lane predicated stores)
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r)
+                        row_fast_lazy<true, NT, true>(
+                            c, rowp[r][0], rowp[r][1], rowp[r][2], rowp[r][3], rowp[r][4],
+                            dbase + (int64_t)(grow0 + r) * g.ld, jbase, bbits[r], st);
+                } else if (dbase) {
                     const uint64_t rstep = (uint64_t)g.ld * sizeof(float);
                     uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * g.ld);
-#ifdef MVM_ROW_PREFETCH
                     // row r + 1's line is read from LDS before row r is
                     // computed (the scheduling barrier keeps the reads there),
-                    // so its LDS latency hides behind row r's arithmetic
+                    // so its LDS latency hides behind row r's arithmetic; the
+                    // row address stays a running scalar (the empty asm stops
+                    // LICM hoisting all RPW row bases out of the chunk loop,
+                    // where they would be spilled to VGPR lanes)
                     double cur[5], nxt[5];
 #pragma unroll
                     for (int e = 0; e < 5; ++e) cur[e] = rowp[0][e];
@@ -467,19 +479,6 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
 #pragma unroll
                         for (int e = 0; e < 5; ++e) cur[e] = nxt[e];
                     }
-#else
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) {
-                        row_fast_lazy<true, NT>(c, rowp[r][0], rowp[r][1], rowp[r][2],
-                                                rowp[r][3], rowp[r][4],
-                                                reinterpret_cast<float *>(rp), jbase, bbits[r]);
-                        rp += rstep;
-                        // keep the row address a running scalar: stops LICM
-                        // hoisting all RPW row bases out of the chunk loop
-                        // (they would be spilled to VGPR lanes)
-                        __asm__ volatile("" : "+s"(rp));
-                    }
-#endif
                 } else {
 #pragma unroll
                     for (int r = 0; r < RPW; ++r)
@@ -487,7 +486,14 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                                                  rowp[r][3], rowp[r][4], nullptr, jbase,
                                                  bbits[r]);
                 }
-            }
+            };
+            // chunks inside the row pitch run without a per-lane test; in the
+            // last chunk of a ragged view the lanes past the pitch store nothing
+            // (their columns hold pad lines: +inf, never a minimum)
+            const int n_full = g.lim / kChunk;
+            int c0 = 0;
+            for (; c0 < nb && c0 < n_full * kChunk; c0 += kChunk) sweep_chunk(c0, std::false_type{});
+            if (c0 < nb) sweep_chunk(c0, std::true_type{});
             constexpr int LPR = kWave / RPW;
             constexpr int VPL = kColsPerLane * (kMaxColTile / kChunk) / LPR;
             static_assert(VPL >= 1 && LPR * VPL == kColsPerLane * (kMaxColTile / kChunk),

@@ -25,7 +25,7 @@ cmd = [G._hipcc(), *flags, "-I" + os.path.join(G.PKG, "csrc"), "--cuda-device-on
        *("-D" + d for d in args.defs), "-o", args.asm or os.devnull, args.src, "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True)
 if out.returncode:
-    sys.exit(out.stderr)
+    sys.exit("\n".join(l for l in out.stderr.splitlines() if "error" in l)[:3000])
 rows, cur = [], None
 for line in out.stderr.splitlines():
     m = re.search(r"remark: (?:\s*)([^:\[]+?): (\S+) \[", line)
