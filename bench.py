@@ -714,7 +714,7 @@ def main():
             cpu["note"] = (f"rank 0 of {world}, after the timed region, on a sample of its own "
                            "scenes; per host, so compare it with the whole-job value")
     traffic = load_traffic(args.workload, chunk)
-    kernel = "pairwise_kernel" if wl["mode"] == "pairwise" else "triplet_fused_kernel"
+    kernel = "pairwise_lazy_kernel" if wl["mode"] == "pairwise" else "triplet_fused_kernel"
     launch_desc = {
         "launch": ("one hipGraph per launch of each timed step (captured once outside the timed "
                    "region), replayed in order; with N > 1 the launch's association gather piece "

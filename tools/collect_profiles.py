@@ -18,8 +18,8 @@ ROUND, SRC = sys.argv[1], sys.argv[2]
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DST = os.path.join(REPO, "profiles", ROUND)
 # the kernel that is one bench launch, per workload
-OP_KERNELS = {"c3": ["pairwise_kernel<16, true, float, 1"],
-              "c2": ["pairwise_kernel<16, true, float, 1"],
+OP_KERNELS = {"c3": ["pairwise_lazy_kernel<16, 1"],
+              "c2": ["pairwise_lazy_kernel<16, 1"],
               "c2cube": ["triplet_fused_kernel"]}
 
 
