@@ -51,6 +51,9 @@ struct PairArgs {
     int32_t lazy;               // 1: association by pairwise_lazy_kernel when the view fits
                                 // one column tile; 0: eager argmin (mvm_options)
     int32_t row_slots;          // lazy kernel: row-line slots per wave in LDS
+    int32_t row_stride;         // lazy kernel: row stride within a wave's row group
+                                // (1 contiguous, kWaves interleaved over the waves)
+    int32_t row_interleave;     // mvm_options.pairwise_row_interleave (host side)
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -334,15 +337,15 @@ __device__ __forceinline__ void load_row_points(const double *pts, int64_t oa, i
     }
 }
 
-// Line {l0, l1, l2, x, y, state} of local row xw + row into `slot` (6 doubles);
-// rows past the view (row >= nrows) get a degenerate record.
+// Line {l0, l1, l2, x, y, state} of the workgroup's local row `lrow` into
+// `slot` (6 doubles); rows past the view (!valid) get a degenerate record.
 __device__ __forceinline__ void put_row_line(double *slot, const double *s_rpt,
-                                             const double (&f)[9], int xw, int row, int nrows) {
+                                             const double (&f)[9], int lrow, bool valid) {
     double l0 = 0, l1 = 0, l2 = 0, x = 0, y = 0;
     bool deg = true;
-    if (row < nrows) {
-        x = s_rpt[2 * (xw + row)];
-        y = s_rpt[2 * (xw + row) + 1];
+    if (valid) {
+        x = s_rpt[2 * lrow];
+        y = s_rpt[2 * lrow + 1];
         deg = row_line(f, x, y, l0, l1, l2);
     }
     slot[0] = l0;
@@ -393,6 +396,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
     float *const dbase = args.dist ? reinterpret_cast<float *>(args.dist) + g.doff : nullptr;
     const bool vec_ok = dbase && ((g.doff & 3) == 0) && ((g.ld & 3) == 0);
     constexpr int U = kWaves * RPW;
+    // a wave's row group: local rows group_base(gi) + r * RST, r < RPW --
+    // contiguous (RST 1), or interleaved over the waves (RST kWaves: at each
+    // row step the four waves store four adjacent rows)
+    const int RST = args.row_stride;
+    auto group_base = [&](int gi) { return RST == 1 ? (gi * kWaves + wave) * RPW : gi * U + wave; };
 
     load_row_points(args.pts, g.oa, na, row0, args.rows_per_wg, s_rpt);
     load_col_lines(args.pts, f, g.ob, nb, 0, T, s_l0, s_l1, s_l2, s_x, s_y, s_cst);
@@ -407,19 +415,18 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
     // every row line up front (one pass instead of one 16-lane pass per group)
     const bool pre = RPW * n_groups <= RS;   // uniform
     if (pre && lane < RPW * n_groups) {
-        const int gi = lane / RPW, slot = lane % RPW;
-        const int xw = (gi * kWaves + wave) * RPW;
-        put_row_line(s_roww + 6 * lane, s_rpt, f, xw, slot, min(RPW, na - (row0 + xw)));
+        const int lrow = group_base(lane / RPW) + (lane % RPW) * RST;
+        put_row_line(s_roww + 6 * lane, s_rpt, f, lrow, row0 + lrow < na);
     }
     for (int gi = 0; gi < n_groups; ++gi) {
-        const int xw = (gi * kWaves + wave) * RPW;
-        const int grow0 = row0 + xw;
-        const int nrows = min(RPW, na - grow0);                 // may be <= 0
+        const int xw = group_base(gi);
+        const int grow0 = row0 + xw;                            // row r: grow0 + r * RST
+        const int nrows = min(RPW, (na - grow0 + RST - 1) / RST);   // may be <= 0
         double(*rowp)[6] = reinterpret_cast<double(*)[6]>(s_roww + (pre ? gi * RPW * 6 : 0));
         if (!pre && lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
             int lz = lane;          // fresh per group: its LDS address is not hoisted and spilled
             __asm__ volatile("" : "+v"(lz));
-            put_row_line(s_roww + 6 * lz, s_rpt, f, xw, lz, nrows);
+            put_row_line(s_roww + 6 * lz, s_rpt, f, xw + lz * RST, lz < nrows);
         }
         if (nrows <= 0) continue;
         // the same wave reads them back (LDS executes one wave's ops in order)
@@ -452,9 +459,9 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                     for (int r = 0; r < RPW; ++r)
                         row_fast_lazy<true, NT, true>(
                             c, rowp[r][0], rowp[r][1], rowp[r][2], rowp[r][3], rowp[r][4],
-                            dbase + (int64_t)(grow0 + r) * g.ld, jbase, bbits[r], st);
+                            dbase + (int64_t)(grow0 + r * RST) * g.ld, jbase, bbits[r], st);
                 } else if (dbase) {
-                    const uint64_t rstep = (uint64_t)g.ld * sizeof(float);
+                    const uint64_t rstep = (uint64_t)g.ld * RST * sizeof(float);
                     uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * g.ld);
                     // row r + 1's line is read from LDS before row r is
                     // computed (the scheduling barrier keeps the reads there),
@@ -542,7 +549,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 }
             }
             if (seg == 0) {
-                const int64_t row = g.row_off0 + grow0 + rs;
+                const int64_t row = g.row_off0 + grow0 + rs * RST;
                 if (args.argmin) args.argmin[row] = jwin;
                 if (args.minval) args.minval[row] = __uint_as_float(k);
             }
@@ -556,7 +563,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
         for (int r = 0; r < nrows; ++r) {
             const double *rl = rowp[r];
             const bool rdeg = __builtin_amdgcn_readfirstlane((int)rl[5]) == (int)kDeg;
-            float *drow = dbase ? dbase + (int64_t)(grow0 + r) * g.ld : nullptr;
+            float *drow = dbase ? dbase + (int64_t)(grow0 + r * RST) * g.ld : nullptr;
             Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
             for (int c0 = 0; c0 < nb; c0 += kChunk) {
                 ColRegs c;
@@ -578,7 +585,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             int32_t imin;
             wave_argmin(best_key(b), b.j, kmin, imin);
             if (lane == 0) {
-                const int64_t row = g.row_off0 + grow0 + r;
+                const int64_t row = g.row_off0 + grow0 + r * RST;
                 if (args.argmin) args.argmin[row] = (kmin == kKeyInvalid) ? -1 : imin;
                 if (args.minval) args.minval[row] = value_of_key(kmin);
             }
@@ -636,7 +643,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
     if (pre && lane < RPW * n_groups) {
         const int gi = lane / RPW, slot = lane % RPW;
         const int xw = (gi * kWaves + wave) * RPW;
-        put_row_line(s_row[wave][lane], s_rpt, f, xw, slot, min(RPW, na - (row0 + xw)));
+        put_row_line(s_row[wave][lane], s_rpt, f, xw + slot, slot < na - (row0 + xw));
     }
     for (int gi = 0; gi < n_groups; ++gi) {
         const int xw = (gi * kWaves + wave) * RPW;
@@ -646,7 +653,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_kernel(PairArgs args) 
         if (!pre && lane < RPW) {   // row lines of this wave's group (wave-private LDS slots)
             int lz = lane;          // fresh per group: its LDS address is not hoisted and spilled
             __asm__ volatile("" : "+v"(lz));
-            put_row_line(s_row[wave][lz], s_rpt, f, xw, lz, nrows);
+            put_row_line(s_row[wave][lz], s_rpt, f, xw + lz, lz < nrows);
         }
         // the same wave reads them back (LDS executes one wave's ops in order)
         const bool rows_fast =
@@ -825,6 +832,12 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     // up-front row-line pass), else one group's.
     if (argmin && !f64 && a.lazy && max_cols <= kMaxColTile) {
         a.row_slots = RPW * row_groups <= kWave ? RPW * row_groups : RPW;
+        // rows interleaved over the waves for views of several chunks (C3:
+        // 4.065 -> 4.034 ms mean over eight output buffers, the gain on the
+        // slow HBM regions); one-chunk views keep contiguous rows (C2: 0.136
+        // vs 0.147 ms interleaved) -- profiles/r03/ab/c*_interleave.log
+        a.row_stride = (a.row_interleave > 0 || (a.row_interleave == 0 && max_cols > kChunk))
+                           ? kWaves : 1;
         const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, a.row_slots, true);
         // LDS for at most two workgroups per CU (C3's 1,024 column lines): the
         // register cap of three waves per SIMD buys nothing there
@@ -836,6 +849,7 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
                     : launch_lds(pairwise_lazy_kernel<RPW, 0>, grid, block, lds, stream, a);
     }
     a.row_slots = kWave;
+    a.row_stride = 1;
     const size_t lds = pairwise_lds_bytes<RPW>(a.col_tile, a.rows_per_wg, kWave, false);
     if (f64) return launch_lds(pairwise_kernel<RPW, false, double>, grid, block, lds, stream, a);
     if (nt) {
@@ -867,6 +881,10 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     const int rpw = o.pairwise_rows_per_wave ? o.pairwise_rows_per_wave : kRowsPerWave;
     if (rpw != 4 && rpw != 8 && rpw != 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_rows_per_wave %d not 4, 8 or 16", rpw);
+    if (o.pairwise_row_interleave < -1 || o.pairwise_row_interleave > 1)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_interleave %d not -1, 0 or 1",
+                        (int)o.pairwise_row_interleave);
+    a.row_interleave = o.pairwise_row_interleave;
     if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
                         (int)o.pairwise_row_groups);

@@ -118,6 +118,11 @@ typedef struct mvm_options {
                                        lsap_reg_max_cols up to this (short sides <= 1024)
                                        over ceil(long / 4096) co-resident workgroups with
                                        the column state in registers (ABI 3) */
+    int32_t pairwise_row_interleave; /* 0 default (by view size: on for views of more
+                                       than 256); 1 a row group's rows interleave over
+                                       the workgroup's 4 waves (at each row step they
+                                       store 4 adjacent rows); -1 each wave's rows
+                                       contiguous (ABI 3) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

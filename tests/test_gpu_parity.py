@@ -54,15 +54,22 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C, options=None):
 
 
 # ----------------------------------------------------------- pairwise ----
-@pytest.fixture(params=["default", "unpitched", "eager", "eager_unpitched", "rpw8_rg2", "rpw4"])
+@pytest.fixture(params=["default", "unpitched", "eager", "eager_unpitched", "rpw8_rg2", "rpw4",
+                        "interleaved", "contiguous", "interleaved_unpitched_rpw8"])
 def argmin_path(request):
     """mvm_options of a pairwise kernel path: the lazy argmin (clean row
     groups: per-chunk minimum bits, column recovered per group through one
     LDS transpose; the default), the eager argmin, other row-group shapes (8
-    rows per wave x 2 groups, 4 rows per wave) -- each with the plan's default
-    row pitch (128-byte lines for ragged views) and the first two also
-    unpitched (rows of n_b, the unaligned-row paths)."""
+    rows per wave x 2 groups, 4 rows per wave), a row group's rows interleaved
+    over the waves or contiguous per wave (forced either way; the default
+    picks by view size) -- each with the plan's default row pitch (128-byte
+    lines for ragged views) and some also unpitched (rows of n_b, the
+    unaligned-row paths)."""
     return {"default": {}, "unpitched": {"_row_align": 1},
+            "interleaved": {"pairwise_row_interleave": 1},
+            "contiguous": {"pairwise_row_interleave": -1},
+            "interleaved_unpitched_rpw8": {"pairwise_row_interleave": 1, "_row_align": 1,
+                                           "pairwise_rows_per_wave": 8},
             "eager": {"pairwise_argmin": "eager"},
             "eager_unpitched": {"pairwise_argmin": "eager", "_row_align": 1},
             "rpw8_rg2": {"pairwise_rows_per_wave": 8, "pairwise_row_groups": 2},

@@ -25,6 +25,9 @@ from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--libs", required=True)
+ap.add_argument("--opts", default="default",
+                help="semicolon list of option sets run with every build: default, or "
+                     "comma-separated mvm_options fields, e.g. 'default;pairwise_row_groups=2'")
 ap.add_argument("--workload", choices=["cube", "c3", "c2"], default="cube")
 ap.add_argument("--buffers", type=int, default=6)
 ap.add_argument("--rounds", type=int, default=3)
@@ -89,6 +92,15 @@ def vmm_buffer(n, chunk_mb):
           f"{size // chunk} chunks at 0x{base.value:x}")
     return torch.as_tensor(DevPtr(base.value, n), device=torch.device("cuda", 0))
 
+def parse_opts(spec):
+    if spec == "default":
+        return None
+    kw = dict(kv.split("=") for kv in spec.split(","))
+    return _native.make_options(**{k: (v if k == "pairwise_argmin" else int(v))
+                                   for k, v in kw.items()})
+
+
+opt_sets = {o: parse_opts(o) for o in args.opts.split(";")}
 libs = {}
 for path in args.libs.split(","):
     lib = ctypes.CDLL(os.path.abspath(path), mode=ctypes.RTLD_LOCAL)
@@ -96,7 +108,8 @@ for path in args.libs.split(","):
         fn = getattr(lib, name, None)   # older builds lack newer entry points
         if fn is not None:
             fn.restype, fn.argtypes = res, argt
-    libs[os.path.basename(path)] = lib
+    for o in opt_sets:   # one column per (build, option set)
+        libs[os.path.basename(path) + ("" if o == "default" else f"[{o}]")] = (lib, opt_sets[o])
 
 dev = torch.device("cuda", 0)
 P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
@@ -117,17 +130,19 @@ mv = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
 stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
-def launch(lib, out):
+def launch(entry, out):
+    lib, opt = entry
+    po = ctypes.byref(opt) if opt is not None else None
     if args.workload == "cube":
         st = lib.mvm_triplet_cost_argmin_ex(P(pts), P(co), P(F), plan.n_scenes, plan.max_n,
                                             P(plan.cube_offs), P(plan.row_offs), P(out), P(am),
                                             P(mv), P(plan.workspace), plan.workspace.numel(),
-                                            None, stream)
+                                            po, stream)
     else:
         st = lib.mvm_pairwise_residual_argmin_ex(P(pts), P(co), P(F), pa, pb, plan.n_scenes,
                                                  plan.n_cams, len(plan.pair_a), plan.max_n,
                                                  P(plan.dist_offs), P(plan.row_offs), P(out),
-                                                 P(am), P(mv), None, stream)
+                                                 P(am), P(mv), po, stream)
     assert st == 0, st
 
 
