@@ -171,6 +171,18 @@ __device__ __forceinline__ double third_q(double s) {
 // true: third_q(s) == RN(s / 3); false: the caller divides
 __device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q); }
 
+// One lane's 16 bytes of a cube row.  `lined`: every row starts on a 128-byte
+// line (P and the scene's offset multiples of 32) -> nontemporal; otherwise a
+// row's first and last lines are shared with its neighbours and the default
+// policy lets L2 merge them (nontemporal partial lines reach HBM as masked
+// writes: 200^3 1.91 -> 1.57 ms, 100^3 1.11 -> 1.06 ms per launch on the same
+// buffers, profiles/r03/ab/cube_partial_lines_*.log).  Uniform per launch.
+__device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[4],
+                                               bool lined) {
+    if (lined) store4_nt_row<1>(base, off, v);
+    else store4_nt_row<0>(base, off, v);
+}
+
 // ------------------------------------------- tiled triplet kernel (v3) ----
 // The 3-camera cube for P <= 256 from the fp64 workspace: a workgroup owns
 // (scene, 16 consecutive j, IB consecutive i).  Its prologue loads everything
@@ -283,8 +295,8 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
                 if (act) {
-                    store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                  (uint32_t)kb * 4u, v);
+                    cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                  (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
                 }
                 Best b{v[0], kb};
 #pragma unroll
@@ -575,8 +587,8 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
 #pragma unroll
                     for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
                     if (act) {
-                        store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                      (uint32_t)kb * 4u, v);
+                        cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                      (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
                     }
                     Best b{v[0], kb};
 #pragma unroll
@@ -904,8 +916,8 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
 #pragma unroll
                         for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
                         if (act) {
-                            store4_nt_row(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
-                                          (uint32_t)kb * 4u, v);
+                            cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
+                                          (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
                         }
                         Best b{v[0], kb};
 #pragma unroll

@@ -122,9 +122,9 @@ def _run_bench(repo, argv, env, tmp_path, name):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_scenes", [24, 25])
-def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
-    """bench.py under torchrun with 2 ranks sharing the one GPU (gloo group):
+@pytest.mark.parametrize("world,n_scenes", [(2, 24), (2, 25), (4, 21), (8, 40)])
+def test_ranks_real_kernel_equal_single_process(tmp_path, world, n_scenes):
+    """bench.py under torchrun with 2 (4, 8) ranks sharing the one GPU (gloo group):
     each rank runs libmvmatch.so's pairwise kernel on its own scene shard, the
     association rows are gathered to rank 0 (chunked async gathers for equal
     shards, the one-shot padded gather for 13 + 12 scenes), and rank 0's
@@ -145,13 +145,13 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
                         env1, tmp_path, "single")
     env2 = dict(env1, MVM_DIST_BACKEND="gloo")
     multi = _run_bench(repo, [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                              "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
-                              "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                              "--nproc-per-node", str(world), "--master-addr", "127.0.0.1",
+                              "--master-port", str(_free_port()), "bench.py", "--gpus", str(world),
                               *common, "--cpu-seconds", "1",
                               "--dump-association", str(tmp_path / "multi")],
                        env2, tmp_path, "multi")
-    assert multi["n_gpus"] == 2
-    assert multi["process_group"]["world_size"] == 2
+    assert multi["n_gpus"] == world
+    assert multi["process_group"]["world_size"] == world
     assert multi["process_group"]["backend"] == "gloo"
     assert multi["config"]["n_scenes_total"] == n_scenes
     assert multi["gather_check"] == "rank-0 rows equal after gather"
@@ -170,7 +170,7 @@ def test_two_ranks_real_kernel_equal_single_process(tmp_path, n_scenes):
     assert rf["achieved"] <= rf["rank0"]["achieved"]
     assert 0 <= multi["step_split"]["exposed_tail_ms"]
     assert multi["step_split"]["exposed_tail_frac"] >= 0
-    assert multi["config"]["launches_per_step"] >= min(5, n_scenes // 2)
+    assert multi["config"]["launches_per_step"] >= min(5, n_scenes // world)
     a1 = np.load(tmp_path / "single" / "argmin.npy")
     m1 = np.load(tmp_path / "single" / "minval.npy")
     a2 = np.load(tmp_path / "multi" / "argmin.npy")
