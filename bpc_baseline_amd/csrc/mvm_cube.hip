@@ -380,8 +380,12 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // splits into SPLIT lane groups of 64/SPLIT lanes, each taking one (i, j) row
 // with lanes along k (4 k per lane), so a wave instruction covers SPLIT rows
 // and no lane idles past P <= 256/SPLIT; a lane computes wave rows
-// r + (8/SPLIT)*(its group).  The argmin of the 8 rows is the transposed
-// butterfly over keys that are invalid outside each row's group.
+// r + (8/SPLIT)*(its group).  A row's argmin is reduced inside its lane
+// group (lane_group_min: DPP within 16-lane rows, an xor-16 swizzle for 32):
+// per row-step 10-12 VALU instead of the 8-row transposed butterfly over the
+// whole wave, which cost more than the row-steps themselves at P <= 64
+// (same buffers: 48^3 2.96 -> 2.26 ms, 64^3 1.92 -> 1.56 ms per 8 GB launch,
+// profiles/r03/ab/cube_group_argmin_*.log).
 template <int kCubeIB, int kCubeRPW, int SPLIT = 1>
 __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr bool HALF = SPLIT > 1;   // split mapping
@@ -619,20 +623,24 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                     idx[r] = b.j;
                 }
             }
-            if constexpr (HALF) {   // SPLIT rows share a wave: keys of the other groups are invalid
-                uint32_t key8[kCubeRPW];
-                int32_t idx8[kCubeRPW];
+            if constexpr (HALF) {
+                // each row lies on one group of kLPR lanes: reduce inside the
+                // groups (key, then the lowest index holding it), then lane g
+                // of group hl stores the group's row g
+                const int g = lane % kLPR;
+                uint32_t mk = kKeyInvalid;
+                int32_t mi = 0x7FFFFFFF;
 #pragma unroll
-                for (int r = 0; r < kCubeRPW; ++r) {
-                    const bool mine = (r / kLaneRows) == hl;
-                    key8[r] = mine ? key[r % kLaneRows] : kKeyInvalid;
-                    idx8[r] = mine ? idx[r % kLaneRows] : 0x7FFFFFFF;
+                for (int r = 0; r < kLaneRows; ++r) {
+                    const uint32_t gk = lane_group_min<kLPR>(key[r]);
+                    const uint32_t gi =
+                        lane_group_min<kLPR>(key[r] == gk ? (uint32_t)idx[r] : 0x7FFFFFFFu);
+                    mk = (g == r) ? gk : mk;
+                    mi = (g == r) ? (int32_t)gi : mi;
                 }
-                uint32_t mk;
-                int32_t mi;
-                wave_argmin8_transposed(key8, idx8, lane, mk, mi);
-                if (lane < nrows) {
-                    const int64_t row = roff + (int64_t)i * M + j0 + lane;
+                const int rr = g + hl * kLaneRows;
+                if (g < kLaneRows && rr < nrows) {
+                    const int64_t row = roff + (int64_t)i * M + j0 + rr;
                     if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
                     if (args.minval) args.minval[row] = value_of_key(mk);
                 }
