@@ -17,7 +17,8 @@ scaling, the default), so ``--gpus 8`` is configs[3]: 1,250 scenes per GPU;
 ``--scaling weak`` gives every rank its own 10,000.  Scenes are processed in
 launches of at most ``--chunk`` scenes, at least ``--min-launches`` per rank
 (5 with N > 1: the gather piece of launch k overlaps launch k+1, so only the
-last piece is exposed); every residual is stored to HBM.  At every N each
+last piece is exposed, and that last launch is a short one, ~1/4 of the
+others); every residual is stored to HBM.  At every N each
 launch of each timed step is a hipGraph captured outside the timed region and
 replayed in order, with N > 1 followed by its gather piece, so the 1 -> N
 curve compares the same launch path (``--graph steps``: one graph for all K
@@ -338,16 +339,22 @@ def load_traffic(workload: str, scenes_per_launch: int):
     return rec
 
 
-def launch_bounds(n_local: int, chunk: int, min_launches: int):
+def launch_bounds(n_local: int, chunk: int, min_launches: int, tail_frac: float = 0.0):
     """[(s0, s1)] scene ranges of a rank's launches: as few as keep each at
     most ``chunk`` scenes, but at least ``min_launches`` (never more than one
     per scene), sizes differing by at most one.  With N > 1 the association
     gather of launch k overlaps launch k+1, so only the last launch's piece is
     exposed: more launches per rank make that tail smaller (configs[3]: 1,250
-    scenes per rank -> 5 x 250, not 2 x 625)."""
+    scenes per rank -> 5 x 250, not 2 x 625).  ``tail_frac`` > 0 adds one
+    short last launch of about that fraction of the others (configs[3]:
+    5 x 238 + 62), so the exposed piece shrinks with it."""
     from bpc_baseline_amd.distributed import shard_range
     n_launch = max(1, -(-n_local // chunk), min(min_launches, n_local))
-    return [shard_range(n_local, k, n_launch) for k in range(n_launch)]
+    tail = 0
+    if tail_frac > 0 and n_local > n_launch:
+        tail = max(1, int(round(n_local / n_launch * tail_frac)))
+    main = [shard_range(n_local - tail, k, n_launch) for k in range(n_launch)]
+    return main + ([(n_local - tail, n_local)] if tail else [])
 
 
 def main():
@@ -412,7 +419,9 @@ def main():
     t0 = time.perf_counter()
     batch = make_scenes(n_local, wl["n_cams"], wl["n_dets"], seed=args.seed, first_scene=first)
     log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
-    bounds = launch_bounds(n_local, wl["chunk"], min_launches)
+    # with N > 1 a short last launch, so the one gather piece no launch
+    # overlaps is small (equal shards: every rank has the same pieces)
+    bounds = launch_bounds(n_local, wl["chunk"], min_launches, 0.25 if world > 1 else 0.0)
     chunk = max(s1 - s0 for s0, s1 in bounds)    # scenes per launch (the largest)
     chunks, n_rows = build_chunks(batch, bounds, dev, wl["mode"])
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)

@@ -420,6 +420,17 @@ def test_bench_launch_split():
     assert sizes(1000, 1000, 1) == [1000]            # C2
     assert sizes(3, 1000, 5) == [1, 1, 1]            # fewer scenes than launches
     assert sizes(12, 8, 5) == [3, 3, 2, 2, 2]
+    # N > 1: a short last launch (its gather piece is the one left exposed)
+    def tapered(n, c, m):
+        b = bench.launch_bounds(n, c, m, 0.25)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(b[k][1] == b[k + 1][0] for k in range(len(b) - 1))
+        return [s1 - s0 for s0, s1 in b]
+    assert tapered(1250, 1000, 5) == [238, 238, 238, 237, 237, 62]   # configs[3]
+    assert tapered(5000, 1000, 5) == [950] * 5 + [250]                # two GPUs
+    assert tapered(3, 1000, 5) == [1, 1, 1]                           # one scene per launch
+    assert tapered(6, 1000, 5) == [1, 1, 1, 1, 1, 1]
+    assert max(tapered(10000, 1000, 5)) <= 1000
     for n, c, m in ((1250, 1000, 8), (7, 2, 3), (10001, 1000, 5), (1, 1, 1)):
         z = sizes(n, c, m)
         assert max(z) <= c and max(z) - min(z) <= 1 and len(z) >= min(m, n)
