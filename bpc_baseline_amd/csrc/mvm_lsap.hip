@@ -438,18 +438,22 @@ __device__ __forceinline__ void lsap_wave_solve(const LsapArgs &a, int p, int64_
     // validate (NaN / -inf, as scipy) and transpose a tall matrix
     int bad = 0;
     {
-        // 8 loads per lane in flight, 32-bit index arithmetic (R * Kc <= 2^20)
+        // kTL loads per lane in flight (32 for the wide classes: 1000 x (576 x 24)
+        // 0.195 -> 0.192 ms, 1000 x (900 x 30) 0.316 -> 0.303 ms against 8,
+        // profiles/r03/lsap/wave_transpose_loads.log), 32-bit index
+        // arithmetic (R * Kc <= 2^20)
+        constexpr int kTL = K >= 8 ? 32 : 8;
         CT *Ctw = reinterpret_cast<CT *>(w + L.ct);   // [nr][nc] = C0^T
         const uint32_t total = (uint32_t)(R * Kc), kc = (uint32_t)Kc;
-        for (uint32_t x0 = lane; x0 < total; x0 += 64 * 8) {
-            CT val[8];
+        for (uint32_t x0 = lane; x0 < total; x0 += 64 * kTL) {
+            CT val[kTL];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < kTL; ++q) {
                 const uint32_t x = x0 + 64u * q;
                 val[q] = x < total ? C0[x] : (CT)0;
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
+            for (int q = 0; q < kTL; ++q) {
                 const uint32_t x = x0 + 64u * q;
                 if (x < total) {
                     bad |= (val[q] != val[q]) || (val[q] == -INFINITY);
