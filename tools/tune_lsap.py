@@ -23,7 +23,9 @@ VARIANTS = {"default": {},
             "wg256": dict(OFF, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
             "wg1024": dict(OFF, lsap_lds_max_cols=-1, lsap_mid_max_cols=-1),
             "nomreg": {"lsap_mreg_max_cols": -1},
-            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1}}
+            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1},
+            "wave512": {"lsap_wave_max_cols": 512, "lsap_multi_g": -1},
+            "wave256": {"lsap_wave_max_cols": 256, "lsap_multi_g": -1}}
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--scenes", type=int, default=1000)
