@@ -183,6 +183,21 @@ __device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, cons
     else store4_nt_row<0>(base, off, v);
 }
 
+// A scene whose third view is empty (P == 0) has no cube entries, but its
+// (i, j) rows still get the association result "no column": argmin -1, minimum
+// NaN (value_of_key(kKeyInvalid); the small and generic kernels' result for
+// such rows, and the oracle's).  Rows i = i_first + i_step * ii (ii < ni) and
+// j in [j0, j0 + nj) of a workgroup's tile; every thread takes a share.
+__device__ __forceinline__ void empty_k_rows(int32_t *argmin, float *minval, int64_t roff, int M,
+                                             int i_first, int i_step, int ni, int j0, int nj) {
+    for (int x = threadIdx.x; x < ni * nj; x += kThreads) {
+        const int ii = x / nj, jj = x - ii * nj;
+        const int64_t row = roff + (int64_t)(i_first + i_step * ii) * M + j0 + jj;
+        if (argmin) argmin[row] = -1;
+        if (minval) minval[row] = value_of_key(kKeyInvalid);
+    }
+}
+
 // ------------------------------------------- tiled triplet kernel (v3) ----
 // The 3-camera cube for P <= 256 from the fp64 workspace: a workgroup owns
 // (scene, 16 consecutive j, IB consecutive i).  Its prologue loads everything
@@ -225,7 +240,12 @@ __global__ __launch_bounds__(kThreads) void triplet_tile_kernel(Cube3Args args) 
     const int P = (int)(args.cam_offs[3 * (int64_t)s + 3] - args.cam_offs[3 * (int64_t)s + 2]);
     const int jw0 = jb * kWaves * kCubeRPW;            // first j of the workgroup
     const int i0 = ib * kCubeIB;
-    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    if (jw0 >= M || i0 >= N) return;                   // uniform over the workgroup
+    if (P == 0) {
+        empty_k_rows(args.argmin, args.minval, args.row_offs[s], M, i0, 1, min(kCubeIB, N - i0),
+                     jw0, min(kWaves * kCubeRPW, M - jw0));
+        return;
+    }
     const int ni = min(kCubeIB, N - i0);
     const int j0 = jw0 + wave * kCubeRPW;              // this wave's first j
     const int nrows = min(kCubeRPW, M - j0);           // may be <= 0 (scalar)
@@ -423,8 +443,13 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
     const int jw0 = jb * kJ;
     const int i_stride = args.i_blocks;                 // tile rows: ib + i_stride * ii
-    if (jw0 >= M || ib >= N || P == 0) return;          // uniform over the workgroup
+    if (jw0 >= M || ib >= N) return;                    // uniform over the workgroup
     const int ni = min(kCubeIB, (N - ib + i_stride - 1) / i_stride);
+    if (P == 0) {
+        empty_k_rows(args.argmin, args.minval, args.row_offs[s], M, ib, i_stride, ni, jw0,
+                     min(kJ, M - jw0));
+        return;
+    }
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
     const int hl = lane / kLPR;                                      // row group of the lane
@@ -778,8 +803,12 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
     const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
     const int jw0 = jb * kJ;
     const int i0 = ib * kCubeIB;
-    if (jw0 >= M || i0 >= N || P == 0) return;         // uniform over the workgroup
+    if (jw0 >= M || i0 >= N) return;                   // uniform over the workgroup
     const int ni = min(kCubeIB, N - i0);
+    if (P == 0) {
+        empty_k_rows(args.argmin, args.minval, args.row_offs[s], M, i0, 1, ni, jw0, min(kJ, M - jw0));
+        return;
+    }
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
     const int kb = kColsPerLane * lane;

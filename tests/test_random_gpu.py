@@ -1,0 +1,146 @@
+"""Seeded random sweep (GPU parity): per-view counts, row pitches, kernel
+options and inputs the fixed-shape tests do not enumerate -- counts on every
+chunk / tile / split boundary (0, 1, 31-33, 255-257, 1023-1025, ...), empty
+views, duplicated detections (argmin ties), half-integer centroids (the
+reference's `_detect`, process_pose.py:133-140), fundamental matrices from the
+synthetic rig, random ones, and ones whose row lines are all degenerate (the
+9999 sentinel, epipolar_matching.py:20-26), plus the odd non-finite centroid.
+Pairwise cases go through the default dispatch with a random row pitch and
+argmin / row-order option, cube cases through each cube kernel path in turn;
+every one is compared with the oracle bit for bit (float32 values as bit
+patterns, indices exactly).  Found on its first run: the tiled cube kernels
+left the association rows of a scene with an empty third view unwritten.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+EDGE_COUNTS = [0, 1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512,
+               513, 1000, 1023, 1024, 1025, 1100]
+CUBE_COUNTS = [0, 1, 2, 5, 16, 31, 32, 33, 44, 45, 48, 63, 64, 65, 100, 127, 128, 129, 200, 256,
+               257, 300]
+
+
+def _bits(a):
+    return np.asarray(a, dtype=np.float32).view(np.int32)
+
+
+def _view(rng, n, nonfinite):
+    """n half-integer centroids in a 2400 x 2400 image, some duplicated."""
+    pts = np.floor(rng.uniform(0.0, 4800.0, size=(n, 2))) / 2.0
+    if n > 1 and rng.random() < 0.5:
+        k = int(rng.integers(1, max(2, n // 4)))
+        pts[rng.integers(0, n, k)] = pts[rng.integers(0, n, k)]
+    if nonfinite and n > 0:
+        pts[rng.integers(0, n), rng.integers(0, 2)] = rng.choice([np.nan, np.inf, -np.inf])
+    return pts
+
+
+def _fundamentals(rng, n_pairs, rig_F):
+    out = np.empty((n_pairs, 9))
+    for p in range(n_pairs):
+        kind = rng.choice(3, p=[0.6, 0.3, 0.1])
+        if kind == 0:
+            out[p] = rig_F[p]
+        elif kind == 1:
+            out[p] = rng.normal(size=9) * rng.choice([1e-6, 1e-3, 1.0])
+        else:
+            f = rng.normal(size=9)
+            f[:6] = 0.0           # row lines (0, 0, c): every one degenerate
+            out[p] = f
+    return out
+
+
+def _batch(rng, S, C, counts_of, nonfinite=False):
+    from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs
+    from bpc_baseline_amd.synth import make_scenes
+    pairs = camera_pairs(C)
+    counts = np.array([[counts_of() for _ in range(C)] for _ in range(S)], np.int64)
+    parts, Fs = [], []
+    for s in range(S):
+        rig = make_scenes(1, C, 1, seed=int(rng.integers(1 << 30))).F
+        Fs.append(_fundamentals(rng, len(pairs), rig))
+        bad = nonfinite and rng.random() < 0.5
+        for c in range(C):
+            parts.append(_view(rng, int(counts[s, c]), bad and c == 0))
+    cam_offs = np.zeros(S * C + 1, np.int64)
+    np.cumsum(counts.reshape(-1), out=cam_offs[1:])
+    pts = np.concatenate(parts) if parts else np.zeros((0, 2))
+    return np.ascontiguousarray(pts), cam_offs, np.ascontiguousarray(np.concatenate(Fs)), pairs
+
+
+@pytest.mark.parametrize("seed", range(64))
+def test_pairwise_random_vs_oracle(cuda, seed):
+    import torch
+    from bpc_baseline_amd import ops
+    rng = np.random.default_rng(7000 + seed)
+    S, C = int(rng.integers(1, 4)), int(rng.integers(2, 5))
+    big = [0]
+
+    def count():
+        # at most two views above 512 per case, so the oracle stays quick
+        c = int(rng.choice(EDGE_COUNTS)) if rng.random() < 0.7 else int(rng.integers(0, 700))
+        if c > 512:
+            if big[0] >= 2:
+                c = int(rng.integers(0, 300))
+            big[0] += 1
+        return c
+
+    pts, cam_offs, F, pairs = _batch(rng, S, C, count, nonfinite=seed % 6 == 5)
+    row_align = rng.choice(["auto", 1, 4, 32, 256])
+    options = [{}, {"pairwise_argmin": "eager"}, {"pairwise_row_interleave": 1},
+               {"pairwise_row_interleave": -1}][int(rng.integers(0, 4))]
+    plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=cuda,
+                            row_align=row_align if row_align == "auto" else int(row_align))
+    d, a, m = ops.pairwise_residual_argmin(
+        torch.from_numpy(pts).to(cuda), torch.from_numpy(cam_offs).to(cuda),
+        torch.from_numpy(F).to(cuda), plan, options=options or None)
+    torch.cuda.synchronize()
+    d = plan.compact(d).cpu().numpy()
+    rd, ra, rm, _, _ = O.pairwise(pts, cam_offs, F, pairs, S, C)
+    what = f"S={S} C={C} counts={np.diff(cam_offs).tolist()} row_align={row_align} {options}"
+    bad = np.nonzero(_bits(d) != _bits(rd))[0]
+    assert bad.size == 0, f"{what}: {bad.size} residual mismatches, first at {bad[:5]}"
+    assert np.array_equal(a.cpu().numpy(), ra), what
+    assert np.array_equal(_bits(m.cpu().numpy()), _bits(rm)), what
+
+
+CUBE_PATHS = [{}, {"cube_kernel": "small"}, {"cube_kernel": "fused"},
+              {"cube_kernel": "fused", "cube_rows_per_instr": 2},
+              {"cube_kernel": "fused", "cube_rows_per_instr": 1}, {"cube_kernel": "workspace"},
+              {"cube_kernel": "generic"}]
+
+
+@pytest.mark.parametrize("seed", range(63))
+def test_cube_random_vs_oracle(cuda, seed):
+    """Every cube kernel path in turn (seed % 7), the default one included."""
+    import torch
+    from bpc_baseline_amd import ops
+    rng = np.random.default_rng(9000 + seed)
+    S = int(rng.integers(1, 4))
+    big = [0]
+
+    def count():
+        c = int(rng.choice(CUBE_COUNTS)) if rng.random() < 0.7 else int(rng.integers(0, 150))
+        if c > 128:
+            if big[0] >= 3:          # one large cube per case at most
+                c = int(rng.integers(0, 64))
+            big[0] += 1
+        return c
+
+    pts, cam_offs, F, _ = _batch(rng, S, 3, count, nonfinite=seed % 5 == 4)
+    options = CUBE_PATHS[seed % len(CUBE_PATHS)]
+    plan = ops.TripletPlan(cam_offs, S, device=cuda)
+    c, a, m = ops.triplet_cost_argmin(torch.from_numpy(pts).to(cuda),
+                                      torch.from_numpy(cam_offs).to(cuda),
+                                      torch.from_numpy(F).to(cuda), plan, options=options or None)
+    torch.cuda.synchronize()
+    rc, ra, rm, _, _ = O.cube(pts, cam_offs, F, S)
+    what = f"S={S} counts={np.diff(cam_offs).tolist()} {options}"
+    bad = np.nonzero(_bits(c.cpu().numpy()) != _bits(rc))[0]
+    assert bad.size == 0, f"{what}: {bad.size} cube mismatches, first at {bad[:5]}"
+    assert np.array_equal(a.cpu().numpy(), ra), what
+    assert np.array_equal(_bits(m.cpu().numpy()), _bits(rm)), what
