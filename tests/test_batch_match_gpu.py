@@ -64,13 +64,19 @@ def _oracle_capture(boxes, conf, cls, offs, K, RT, conf_thresh, thr):
     return out
 
 
-def test_batch_vs_oracle_synthetic(cuda):
+@pytest.mark.parametrize("sizes", ["ipd", "large"])
+def test_batch_vs_oracle_synthetic(cuda, sizes):
+    """ipd: views of 0-40 detections (the small cube kernel, the one-wave
+    assignment); large: 0-100 (the tiled cube kernels -- with empty views
+    among them -- and the wider assignment classes)."""
     from bpc_baseline_amd.synth import make_capture
-    rng = np.random.default_rng(11)
-    S = 120
+    rng = np.random.default_rng(11 if sizes == "ipd" else 12)
+    S = 120 if sizes == "ipd" else 30
+    choices, probs = (([0, 1, 2, 6, 12, 24, 40], [.04, .06, .1, .3, .3, .1, .1]) if sizes == "ipd"
+                      else ([0, 1, 24, 45, 64, 100], [.1, .05, .15, .25, .25, .2]))
     per_image, Ks, RTs = [], [], []
     for s in range(S):
-        counts = list(rng.choice([0, 1, 2, 6, 12, 24, 40], 3, p=[.04, .06, .1, .3, .3, .1, .1]))
+        counts = list(rng.choice(choices, 3, p=probs))
         K, RT, dets = make_capture(rng, 3, counts, duplicates=int(s % 7 == 0))
         for cam in range(3):
             b = np.asarray([d["bbox"] for d in dets[cam]], np.float64).reshape(-1, 4)
@@ -103,6 +109,8 @@ def test_batch_vs_oracle_synthetic(cuda):
             np.testing.assert_allclose(gt, rt, rtol=DLT_RTOL, atol=DLT_ATOL)
         total += len(ref)
     assert total > 2 * S     # the synthetic objects are actually recovered
+    if sizes == "large":
+        return
     # a static rig: F and P passed in give the same results
     from bpc_baseline_amd.inference.batch_match import match_captures, projection_matrices
     from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs, fundamental_matrices_batched

@@ -144,3 +144,57 @@ def test_cube_random_vs_oracle(cuda, seed):
     assert bad.size == 0, f"{what}: {bad.size} cube mismatches, first at {bad[:5]}"
     assert np.array_equal(a.cpu().numpy(), ra), what
     assert np.array_equal(_bits(m.cpu().numpy()), _bits(rm)), what
+
+
+LSAP_EDGES = [1, 2, 3, 24, 63, 64, 65, 128, 129, 256, 257, 512, 513, 576, 768, 769, 1024, 1025,
+              2048, 4096, 4097]
+
+
+@pytest.mark.parametrize("seed", range(36))
+def test_lsap_random_vs_scipy(cuda, seed):
+    """Batched assignment == scipy.optimize.linear_sum_assignment on ragged
+    batches of random shapes around every kernel-class boundary, with ties
+    (half-integer and repeated costs), forbidden (+inf) entries that keep the
+    problem feasible, and float64 or float32 costs (epipolar_matching.py:106-107)."""
+    import torch
+    from scipy.optimize import linear_sum_assignment as scipy_lsa
+    from bpc_baseline_amd import ops
+    rng = np.random.default_rng(11000 + seed)
+    dtype = np.float64 if seed % 3 == 2 else np.float32
+    mats = []
+    for _ in range(int(rng.integers(3, 9))):
+        long_side = int(rng.choice(LSAP_EDGES)) if rng.random() < 0.7 else int(rng.integers(1, 3000))
+        short = int(rng.integers(1, min(long_side, 64) + 1))
+        shape = (long_side, short) if rng.random() < 0.5 else (short, long_side)
+        c = rng.normal(size=shape)
+        if rng.random() < 0.5:
+            c = np.round(c * 4) / 4                       # ties
+        if rng.random() < 0.3:
+            c[:, : max(1, shape[1] // 3)] = c[:, :1]      # repeated columns
+        if rng.random() < 0.4:
+            # forbid entries but keep a feasible diagonal-ish assignment
+            mask = rng.random(shape) < 0.3
+            k = min(shape)
+            keep = (np.arange(k), rng.permutation(shape[1])[:k]) if shape[0] <= shape[1] \
+                else (rng.permutation(shape[0])[:k], np.arange(k))
+            mask[keep] = False
+            c[mask] = np.inf
+        mats.append(c.astype(dtype))
+    tdt = torch.float64 if dtype == np.float64 else torch.float32
+    plan = ops.LsapPlan([m.shape[0] for m in mats], [m.shape[1] for m in mats], device=cuda,
+                        dtype=tdt)
+    flat = np.concatenate([m.reshape(-1) for m in mats] + [np.zeros(1, dtype)])
+    offs = np.zeros(len(mats), np.int64)
+    np.cumsum([m.size for m in mats[:-1]], out=offs[1:])
+    opts = [None, {"lsap_wave_max_cols": -1, "lsap_multi_g": -1},
+            {"lsap_reg_max_cols": -1, "lsap_wave_max_cols": -1, "lsap_multi_g": -1}][seed % 3]
+    r, c, st = ops.linear_sum_assignment_batched(torch.from_numpy(flat).to(cuda),
+                                                 torch.from_numpy(offs).to(cuda), plan,
+                                                 options=opts)
+    r, c, st = r.cpu().numpy(), c.cpu().numpy(), st.cpu().numpy()
+    o = plan.out_offs_host
+    for k, m in enumerate(mats):
+        r0, c0 = scipy_lsa(m)
+        what = f"problem {k} of {[x.shape for x in mats]} ({dtype.__name__}, {opts})"
+        assert int(st[k]) == 0, what
+        assert np.array_equal(r[o[k]:o[k + 1]], r0) and np.array_equal(c[o[k]:o[k + 1]], c0), what
