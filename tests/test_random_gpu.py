@@ -204,3 +204,36 @@ def test_lsap_random_vs_scipy(cuda, seed):
         what = f"problem {k} of {[x.shape for x in mats]} ({dtype.__name__}, {opts})"
         assert int(st[k]) == 0, what
         assert np.array_equal(r[o[k]:o[k + 1]], r0) and np.array_equal(c[o[k]:o[k + 1]], c0), what
+
+
+def test_large_views_pairwise(cuda):
+    """Views far beyond the configurations' (40,000 and 33,333 detections: a
+    6.4 GB and a 5.3 GB matrix in one launch, 40 column tiles per row): the
+    association of every row equals the oracle's, and sampled rows of the
+    matrices are bit-exact (a row depends only on its own point, the other
+    view and F, so the oracle recomputes just those rows)."""
+    import torch
+    from bpc_baseline_amd import ops
+    from bpc_baseline_amd.synth import make_scenes
+    rng = np.random.default_rng(5)
+    counts = [40000, 40000, 33333]
+    b = make_scenes(1, 3, 1, seed=3)
+    pts = np.concatenate([np.floor(rng.uniform(0, 4800, (n, 2))) / 2 for n in counts])
+    cam_offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+    pairs = b.pairs
+    plan = ops.PairwisePlan(cam_offs, 1, 3, pairs, device=cuda)
+    d, a, m = ops.pairwise_residual_argmin(torch.from_numpy(pts).to(cuda),
+                                           torch.from_numpy(cam_offs).to(cuda),
+                                           torch.from_numpy(b.F).to(cuda), plan)
+    torch.cuda.synchronize()
+    _, ra, rm, _, row_offs = O.pairwise(pts, cam_offs, b.F, pairs, 1, 3, want_dist=False)
+    assert np.array_equal(a.cpu().numpy(), ra)
+    assert np.array_equal(_bits(m.cpu().numpy()), _bits(rm))
+    for p, (va, vb) in enumerate(pairs):
+        rows = np.sort(rng.choice(counts[va], 24, replace=False))
+        mat = plan.matrix(d, 0, p)                       # [n_a, n_b] view (pitched rows)
+        got = mat[torch.from_numpy(rows).to(cuda)].cpu().numpy()
+        sub = np.concatenate([pts[cam_offs[va] + rows], pts[cam_offs[vb]:cam_offs[vb + 1]]])
+        sub_offs = np.array([0, len(rows), len(sub)], np.int64)
+        rd, _, _, _, _ = O.pairwise(sub, sub_offs, b.F[p:p + 1], np.array([[0, 1]], np.int32), 1, 2)
+        assert np.array_equal(_bits(got.reshape(-1)), _bits(rd)), f"pair {p}"
