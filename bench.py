@@ -49,10 +49,11 @@ import torch
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from bpc_baseline_amd import ops  # noqa: E402
 from bpc_baseline_amd.distributed import (ChunkedRowGather, gather_rows, init_from_env,  # noqa: E402
                                           max_over_ranks, sum_over_ranks)
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
+
+ops = None   # bpc_baseline_amd.ops, imported by main() once this process is a rank
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "detection-pairs matched/sec"
@@ -109,7 +110,7 @@ def build_chunks(batch, bounds, device, mode):
         pts = pts_all[base:int(co[-1])]
         F = F_all[s0 * P:s1 * P]
         if mode == "pairwise":
-            plan = ops.PairwisePlan(co_rel, s1 - s0, C, batch.pairs, device=device)
+            plan = ops.PairwisePlan(co_rel, s1 - s0, C, batch.pairs, device=device, row_align="auto")
             units, size = int(plan.n_dist), int(plan.dist_size)
             nbytes = pairwise_bytes(counts[s0:s1], batch.pairs)
         else:
@@ -357,6 +358,38 @@ def launch_bounds(n_local: int, chunk: int, min_launches: int, tail_frac: float 
     return main + ([(n_local - tail, n_local)] if tail else [])
 
 
+def launch_ranks(n: int) -> int:
+    """``--gpus N`` (N > 1) started without a launcher: run this same command
+    as N ranks under torchrun in a CHILD process (this parent has made no GPU
+    call and makes none), its output streamed through, and return its exit
+    code.  Rendezvous on 127.0.0.1, one rank per GPU (each rank checks that)."""
+    import signal
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC (RCCL)
+    if "OMP_NUM_THREADS" not in env:                     # torchrun would set 1
+        env["OMP_NUM_THREADS"] = str(max(1, min(16, cpu_threads() // n)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    log(f"launching {n} ranks: {' '.join(cmd)}")
+    proc = subprocess.Popen(cmd, env=env)
+
+    def forward(signum, _frame):
+        proc.send_signal(signum)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
+    rc = proc.wait()
+    if rc != 0:
+        log(f"error: the {n}-rank run exited with status {rc}")
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -388,7 +421,38 @@ def main():
                          "piece of launch k issued right after its replay; steps: one hipGraph "
                          "holding all K steps (one GPU only: a step with N > 1 has collectives); "
                          "off: eager op calls")
+    ap.add_argument("--parity", choices=["full", "scene"], default="full",
+                    help="full (default): after timing, every association row of the last step "
+                         "(all ranks' rows, as gathered to rank 0) against the oracle, which each "
+                         "rank computes for its own scenes and sends to rank 0 over a gloo group; "
+                         "scene: only the last launch's first scene")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="start the ranks and the process group (gloo, host only) and print the "
+                         "world each rank joined; no GPU work (tests the launcher on a CPU host)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit(f"error: --gpus {args.gpus}")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        raise SystemExit(launch_ranks(args.gpus))
+    env_world = int(os.environ.get("WORLD_SIZE", "1"))
+    if env_world != args.gpus:
+        raise SystemExit(f"error: --gpus {args.gpus} but WORLD_SIZE={env_world} (run `python "
+                         "bench.py --gpus N` alone, or under torchrun with --nproc-per-node N)")
+    if args.dry_run:
+        env = init_from_env(backend="gloo", use_gpu=False)
+        seen = gather_rows(env, torch.tensor([env.rank], dtype=torch.int64))
+        if env.world != args.gpus:
+            raise SystemExit(f"error: --gpus {args.gpus} but the process group has {env.world} rank(s)")
+        if env.is_root:
+            print(json.dumps({"dry_run": True, "n_gpus": env.world,
+                              "ranks_seen": [int(x) for x in seen[0]],
+                              "process_group": {"world_size": env.world, "backend": env.backend}
+                              if env.initialised else None}), flush=True)
+        return
+
+    global ops
+    from bpc_baseline_amd import ops as _ops
+    ops = _ops
 
     wl = dict(WORKLOADS[args.workload])
     if args.scenes:
@@ -399,7 +463,11 @@ def main():
     env = init_from_env()
     world = env.world
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}")
+        raise SystemExit(f"error: --gpus {args.gpus} but the process group has {world} rank(s) "
+                         "(run `python bench.py --gpus N` alone, or under torchrun with "
+                         "--nproc-per-node N)")
+    if env.backend == "nccl" and torch.cuda.device_count() < world:
+        raise SystemExit(f"error: {world} RCCL ranks but {torch.cuda.device_count()} visible GPU(s)")
     dev = env.device
     if args.graph == "steps" and env.initialised:
         raise SystemExit("--graph steps needs a single GPU without a process group "
@@ -496,15 +564,17 @@ def main():
     # launch path; "steps" (one GPU): one graph holding all K steps.  Captured
     # thread-locally: the RCCL watchdog thread queries events meanwhile.
     graphs, step_graph = None, None
+    graph_slot = {}       # (step, launch) -> the output slot its graph writes
     cap_kw = dict(capture_error_mode="thread_local")
     if args.graph == "launch":
         graphs = []
-        for _ in range(args.steps):
+        for s in range(args.steps):
             row = []
-            for c in chunks:
+            for k, c in enumerate(chunks):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, **cap_kw):
                     launch(c)
+                graph_slot[(s, k)] = last_slot[id(c)]
                 row.append(g)
             graphs.append(row)
         for row in graphs:                      # first replay uploads the graph: untimed
@@ -522,20 +592,22 @@ def main():
     torch.cuda.synchronize(dev)
     seq[0] = 0
 
-    def run_launch(s: int, k: int):
+    def run_launch(s: int, k: int) -> int:
+        """Run launch k of timed step s; returns the output slot it wrote."""
         if graphs is not None:
             graphs[s][k].replay()
             dispatched[0] += 1
-        else:
-            launch(chunks[k])
+            return graph_slot[(s, k)]
+        launch(chunks[k])
+        return last_slot[id(chunks[k])]
 
     def timed_step(s, events, tails):
         for k, c in enumerate(chunks):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(stream)
-            run_launch(s, k)
+            slot = run_launch(s, k)
             e1.record(stream)
-            events.append((e0, e1, c.nbytes, c.units, 1))
+            events.append((e0, e1, c.nbytes, c.units, 1, slot))
             if overlap:
                 gatherer.issue(k)
         ec, es = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -559,7 +631,7 @@ def main():
             ev1.record(stream)
             dispatched[0] += args.steps * len(chunks)
             events.append((ev0, ev1, sum(c.nbytes for c in chunks) * args.steps,
-                           units_local * args.steps, len(chunks) * args.steps))
+                           units_local * args.steps, len(chunks) * args.steps, None))
         else:
             for s in range(args.steps):
                 gathered = timed_step(s, events, tails)
@@ -611,20 +683,74 @@ def main():
     # ---- kernel roofline from the events (on the launch stream) ------------
     # (with the "steps" graph, one event pair brackets the K steps' launches)
     durs = np.array([e0.elapsed_time(e1) * 1e-3 for e0, e1, *_ in events])
-    byts = np.array([b for _, _, b, _, _ in events], dtype=np.float64)
-    units_ev = np.array([u for _, _, _, u, _ in events], dtype=np.float64)
-    n_launch = sum(n for *_, n in events)
+    byts = np.array([ev[2] for ev in events], dtype=np.float64)
+    units_ev = np.array([ev[3] for ev in events], dtype=np.float64)
+    n_launch = sum(ev[4] for ev in events)
+    # rank 0's launches per output allocation: the same launch runs at
+    # different speeds on different HBM allocations
+    per_slot = None
+    if events and events[0][5] is not None:
+        per_slot = []
+        for sl in sorted({ev[5] for ev in events}):
+            idx = [i for i, ev in enumerate(events) if ev[5] == sl]
+            t = float(durs[idx].sum())
+            per_slot.append({"slot": sl, "launches": len(idx),
+                             "mean_ms": t / len(idx) * 1e3,
+                             "achieved_gbs": float(byts[idx].sum()) / t / 1e9})
+        rates = [p["achieved_gbs"] for p in per_slot]
+        per_slot = {"slots": per_slot, "fastest_over_slowest": max(rates) / min(rates),
+                    "note": "rank 0, HIP events per launch grouped by the output allocation "
+                            "the launch wrote (achieved = algorithmic bytes / time)"}
     avg_dur = float(durs.sum() / n_launch)
     achieved_gbs = float(byts.sum() / durs.sum() / 1e9)
     # every rank's figure, then the slowest rank's (max launch time, min GB/s)
     avg_dur_max = max_over_ranks(env, avg_dur)
     achieved_min = -max_over_ranks(env, -achieved_gbs)
 
-    # ---- the gathered association holds rank 0's rows first (N > 1) -------
-    gather_check = None
-    if env.initialised and env.is_root and gathered is not None:
-        g_am = gathered[0].reshape(-1)[:n_rows].to(argmin.device)
-        gather_check = "rank-0 rows equal after gather" if torch.equal(g_am, argmin) else "MISMATCH"
+    # ---- the whole step's association vs the oracle (untimed) --------------
+    # Every rank runs the oracle (C/OpenMP, oracle/) over its own scenes and
+    # sends the rows to rank 0 over a gloo group (host memory, not the RCCL
+    # transport under test); rank 0 compares them with every row it holds
+    # after the step's gather: rank 0's own rows and what ranks 1..N-1 sent.
+    parity_rows, parity_detail = None, None
+    if args.parity == "full":
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        nth = cpu_threads()
+        if wl["mode"] == "pairwise":
+            _, ra, rm, _, _ = O.pairwise(batch.pts, batch.cam_offs, batch.F, batch.pairs,
+                                         batch.n_scenes, batch.n_cams, want_dist=False, nthreads=nth)
+        else:
+            _, ra, rm, _, _ = O.cube(batch.pts, batch.cam_offs, batch.F, batch.n_scenes,
+                                     want_cube=False, nthreads=nth)
+        t_oracle = max_over_ranks(env, time.perf_counter() - t0)
+        ref = gather_rows(env, torch.from_numpy(ra), torch.from_numpy(rm), group=env.cpu_group())
+        if env.is_root:
+            if env.initialised:
+                g_am, g_mv = (g.reshape(-1).cpu().numpy() for g in gathered[:2])
+            else:
+                g_am, g_mv = argmin.cpu().numpy(), minval.cpu().numpy()
+            r_am, r_mv = ref[0].numpy(), ref[1].numpy()
+            total = int(r_am.size)
+            if g_am.size != total:
+                ok_rows, first_bad = 0, 0
+            else:
+                eq = (g_am == r_am) & (g_mv.view(np.int32) == r_mv.view(np.int32))
+                ok_rows = int(eq.sum())
+                bad = np.flatnonzero(~eq)
+                first_bad = int(bad[0]) if bad.size else None
+            parity_rows = f"{ok_rows}/{total} bit-exact vs oracle"
+            parity_detail = {
+                "rows_checked": total, "rows_bit_exact": ok_rows, "gathered_rows": int(g_am.size),
+                "first_mismatch_row": first_bad, "ranks": world, "oracle_threads_per_rank": nth,
+                "oracle_s": t_oracle,
+                "what": ("every (argmin, min) row of the last timed step, in global scene order: "
+                         + ("rank 0's rows and the rows ranks 1..N-1 sent over the step's gather "
+                            f"({env.backend}), against the oracle rows each rank computed for "
+                            "its own scenes and sent over a gloo group"
+                            if env.initialised else
+                            "the GPU's rows against the oracle's for the same scenes")),
+                "oracle": "oracle/mvm_oracle.c (the reference's epipolar_error + np.argmin rule)"}
     if args.dump_association and env.is_root:
         os.makedirs(args.dump_association, exist_ok=True)
         if env.initialised:
@@ -801,12 +927,17 @@ def main():
         "cpu_baseline": cpu,
         "pcie_inclusive": pcie,
         "parity": parity,
+        "parity_rows": parity_rows,
+        "parity_rows_detail": parity_detail,
     }
-    if gather_check:
-        out["gather_check"] = gather_check
+    if per_slot:
+        out["roofline"]["per_slot"] = per_slot
     if traffic:
         out["roofline"]["traffic_source"] = traffic.get("source")
     print(json.dumps(out), flush=True)
+    if parity_detail and parity_detail["rows_bit_exact"] != parity_detail["rows_checked"]:
+        log(f"error: association parity {parity_rows}")
+        raise SystemExit(3)
 
 
 if __name__ == "__main__":

@@ -12,6 +12,7 @@ on 127.0.0.1).
 """
 from __future__ import annotations
 
+import datetime
 import os
 from typing import List, Optional, Tuple
 
@@ -19,7 +20,12 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["DistEnv", "init_from_env", "shard_range", "gather_rows", "max_over_ranks",
-           "sum_over_ranks", "ChunkedRowGather"]
+           "sum_over_ranks", "ChunkedRowGather", "DEFAULT_TIMEOUT_S"]
+
+# every collective (RCCL or gloo) of a process group made here fails after
+# this long instead of hanging the job: a stuck gather on an 8-GPU run ends
+# the run non-zero with a message (MVM_DIST_TIMEOUT_S overrides it)
+DEFAULT_TIMEOUT_S = 300
 
 
 class DistEnv:
@@ -27,6 +33,18 @@ class DistEnv:
                  initialised: bool, backend: Optional[str] = None):
         self.rank, self.world, self.local_rank = rank, world, local_rank
         self.device, self.initialised, self.backend = device, initialised, backend
+        self._cpu_group = None
+        self.timeout = datetime.timedelta(seconds=DEFAULT_TIMEOUT_S)
+
+    def cpu_group(self):
+        """A gloo group over the same ranks, for host-memory collectives next
+        to an RCCL default group (collective: every rank must call it, in the
+        same order).  None when the default group is already gloo."""
+        if not self.initialised or self.backend == "gloo":
+            return None
+        if self._cpu_group is None:
+            self._cpu_group = dist.new_group(backend="gloo", timeout=self.timeout)
+        return self._cpu_group
 
     @property
     def is_root(self) -> bool:
@@ -40,24 +58,33 @@ class DistEnv:
                 dist.barrier()
 
 
-def init_from_env(backend: Optional[str] = None, use_gpu: bool = True) -> DistEnv:
+def init_from_env(backend: Optional[str] = None, use_gpu: bool = True,
+                  timeout_s: Optional[float] = None) -> DistEnv:
     """Initialise torch.distributed from torchrun's env (single process if absent).
 
     One process per GPU: rank -> cuda:LOCAL_RANK.  ``backend`` defaults to
     "nccl" (RCCL over xGMI on ROCm) for GPU ranks and "gloo" otherwise;
     MVM_DIST_BACKEND overrides it (gloo rehearsals of several ranks on one
-    GPU map LOCAL_RANK onto the visible devices round-robin)."""
+    GPU map LOCAL_RANK onto the visible devices round-robin).  Collectives
+    time out after ``timeout_s`` (default MVM_DIST_TIMEOUT_S or 300 s); an
+    RCCL rank with no GPU of its own raises."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("MVM_DIST_BACKEND") or backend or ("nccl" if use_gpu else "gloo")
     if use_gpu:
         n_dev = torch.cuda.device_count()
+        if backend == "nccl" and local_rank >= n_dev:
+            raise RuntimeError(f"rank {rank}: LOCAL_RANK {local_rank} but only {n_dev} visible GPU(s); "
+                               "RCCL needs one GPU per rank")
         index = local_rank % n_dev if (backend == "gloo" and n_dev) else local_rank
         torch.cuda.set_device(index)
         device = torch.device("cuda", index)
     else:
         device = torch.device("cpu")
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("MVM_DIST_TIMEOUT_S", DEFAULT_TIMEOUT_S))
+    timeout = datetime.timedelta(seconds=timeout_s)
     initialised = False
     # MVM_DIST_FORCE=1 creates the process group even for one rank, so the
     # RCCL code path (device-bound group, async gathers) runs on a 1-GPU box
@@ -65,12 +92,14 @@ def init_from_env(backend: Optional[str] = None, use_gpu: bool = True) -> DistEn
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         kw = {"device_id": device} if (use_gpu and backend == "nccl") else {}
-        dist.init_process_group(backend=backend, rank=rank, world_size=world, **kw)
+        dist.init_process_group(backend=backend, rank=rank, world_size=world, timeout=timeout, **kw)
         initialised = True
         # what the process group itself reports, not what the launcher's env said
         world, rank = dist.get_world_size(), dist.get_rank()
         backend = str(dist.get_backend())
-    return DistEnv(rank, world, local_rank, device, initialised, backend)
+    env = DistEnv(rank, world, local_rank, device, initialised, backend)
+    env.timeout = timeout
+    return env
 
 
 def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
@@ -80,17 +109,20 @@ def shard_range(n_items: int, rank: int, world: int) -> Tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
-def gather_rows(env: DistEnv, *tensors: torch.Tensor) -> Optional[List[torch.Tensor]]:
+def gather_rows(env: DistEnv, *tensors: torch.Tensor, group=None) -> Optional[List[torch.Tensor]]:
     """Gather equally-shaped 1-D per-rank tensors to rank 0 (concatenated in rank
     order).  Ragged shards are padded to the largest shard and trimmed on rank 0.
-    Returns the gathered tensors on rank 0, None elsewhere; identity at world 1."""
+    Returns the gathered tensors on rank 0, None elsewhere; identity at world 1.
+    ``group``: a gloo group (``env.cpu_group()``) to gather host tensors over
+    instead of the default group."""
     if not env.initialised:
         return list(tensors)
-    if env.backend == "gloo" and tensors[0].device.type != "cpu":
+    on_host = group is not None or env.backend == "gloo"
+    if on_host and tensors[0].device.type != "cpu":
         tensors = tuple(t.cpu() for t in tensors)   # gloo collectives run on host memory
     n_local = torch.tensor([tensors[0].numel()], dtype=torch.int64, device=tensors[0].device)
     sizes = [torch.zeros_like(n_local) for _ in range(env.world)]
-    dist.all_gather(sizes, n_local)
+    dist.all_gather(sizes, n_local, group=group)
     sizes = [int(s.item()) for s in sizes]
     n_max = max(sizes)
     out = []
@@ -99,7 +131,7 @@ def gather_rows(env: DistEnv, *tensors: torch.Tensor) -> Optional[List[torch.Ten
             pad = torch.zeros(n_max - t.numel(), dtype=t.dtype, device=t.device)
             t = torch.cat([t, pad])
         bufs = [torch.empty_like(t) for _ in range(env.world)] if env.is_root else None
-        dist.gather(t.contiguous(), gather_list=bufs, dst=0)
+        dist.gather(t.contiguous(), gather_list=bufs, dst=0, group=group)
         if env.is_root:
             out.append(torch.cat([b[:n] for b, n in zip(bufs, sizes)]))
     return out if env.is_root else None

@@ -165,13 +165,17 @@ _POOL = {}
 
 
 def rig_worker_pool(n: int):
-    """The process-wide ``RigWorkers`` of ``n`` processes (started on first use,
-    reused by every stream, closed at exit)."""
+    """The calling thread's ``RigWorkers`` of ``n`` processes (started on first
+    use, reused by every stream of that thread, closed at exit).  Per thread:
+    a pool has one job in flight, and two threads streaming at once must not
+    share it."""
+    import threading
     from .rig_workers import RigWorkers
-    pool = _POOL.get(n)
-    if pool is None:
+    key = (threading.get_ident(), n)
+    pool = _POOL.get(key)
+    if pool is None or not pool.procs:      # first use, or closed (thread ids are reused)
         import atexit
-        pool = _POOL[n] = RigWorkers(n)
+        pool = _POOL[key] = RigWorkers(n)
         atexit.register(pool.close)
     return pool
 
@@ -195,14 +199,20 @@ def match_capture_stream(batches: Iterable[Sequence], *, rig_workers: int = 3,
     if cur is None:
         return
     pool = rig_worker_pool(rig_workers) if rig_workers > 0 else None
-    if pool is not None:
-        pool.submit(*_rig_inputs(cur))
-    while cur is not None:
-        F_h, P_h = pool.result() if pool is not None else rig_matrices(*_rig_inputs(cur))
-        nxt = next(it, None)
-        if nxt is not None and pool is not None:
-            pool.submit(*_rig_inputs(nxt))       # batch b+1's F/P while batch b runs
-        dev = cur[0].device
-        yield match_captures(*cur, F=torch.from_numpy(F_h).to(dev),
-                             proj=torch.from_numpy(P_h).to(dev), **kwargs)
-        cur = nxt
+    try:
+        ticket = pool.submit(*_rig_inputs(cur)) if pool is not None else None
+        while cur is not None:
+            F_h, P_h = pool.result(ticket) if pool is not None else rig_matrices(*_rig_inputs(cur))
+            nxt = next(it, None)
+            if nxt is not None and pool is not None:
+                ticket = pool.submit(*_rig_inputs(nxt))   # batch b+1's F/P while batch b runs
+            dev = cur[0].device
+            yield match_captures(*cur, F=torch.from_numpy(F_h).to(dev),
+                                 proj=torch.from_numpy(P_h).to(dev), **kwargs)
+            cur = nxt
+    finally:
+        # a consumer that stops early (break, exception, the generator
+        # collected) leaves batch b+1's job in flight: collect it, so the
+        # thread's pool takes the next stream's submit
+        if pool is not None:
+            pool.drain()

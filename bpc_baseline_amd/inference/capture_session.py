@@ -110,9 +110,15 @@ class _Staging:
     def ptr(self, name: str):
         return _vp(self.dev, self.offs[name][0])
 
-    def upload(self, upto: str = None) -> None:
-        n = self.nbytes if upto is None else self.offs[upto][0] + (
-            np.dtype(self.offs[upto][1]).itemsize * self.offs[upto][2])
+    def upload(self, upto: str = None, count: Optional[int] = None) -> None:
+        """Copy the regions from the start through ``upto`` (all when None);
+        ``count``: only the first ``count`` elements of ``upto`` itself."""
+        if upto is None:
+            n = self.nbytes
+        else:
+            o, dt, cap = self.offs[upto]
+            n = o + np.dtype(dt).itemsize * (cap if count is None else min(int(count), cap))
+        n = max(n, 1)
         self.dev[:n].copy_(self.host[:n], non_blocking=True)
 
 
@@ -223,7 +229,7 @@ class LsapSlot:
         np.copyto(st.np["cost"][:rows * cols], cost.reshape(-1))
         cs = torch.cuda.current_stream(self.dev)
         stream = ctypes.c_void_p(cs.cuda_stream)
-        st.upload()
+        st.upload("cost", rows * cols)     # the cost region is last: skip its unused tail
         long_side = max(rows, cols)
         rc = _native.load().mvm_lsap_solve_ex(
             st.ptr("cost"), self.code, st.ptr("cost_offs"), st.ptr("dims"), 1, st.ptr("ws_offs"),

@@ -13,10 +13,15 @@ captures.  Inputs (Ks, RTs) and outputs (F, P) travel through shared memory;
 a job is one short text line per worker over its stdin, answered on stdout.  ``submit`` returns at once;
 ``result`` waits and returns copies, so a pipeline can submit batch b+1
 before it runs batch b.  Two shared-memory slots alternate, so one job may be
-in flight while the previous job's result is read.
+in flight while the previous job's result is read.  One job is in flight at a
+time per pool: ``submit`` returns a ticket that ``result`` checks, and a lock
+keeps two threads from interleaving the pool's state (each thread should hold
+its own pool, as ``batch_match.rig_worker_pool`` gives it).
 """
 from __future__ import annotations
 
+import itertools
+import threading
 from multiprocessing import shared_memory
 from typing import List, Optional, Tuple
 
@@ -127,7 +132,9 @@ class RigWorkers:
                       for _ in range(max(1, int(n)))]
         self.slots: List[Optional[_Slot]] = [None, None]
         self.next_slot = 0
-        self.pending = None               # (slot index, S, workers used)
+        self.pending = None               # (ticket, slot index, S, workers used)
+        self._tickets = itertools.count(1)
+        self._lock = threading.Lock()
 
     def _send(self, w: int, line: str) -> None:
         self.procs[w].stdin.write(line + "\n")
@@ -145,8 +152,15 @@ class RigWorkers:
             self.slots[k] = _Slot(max(S, 1))
         return k
 
-    def submit(self, Ks: np.ndarray, RTs: np.ndarray) -> None:
-        """Start computing F/P of one batch (Ks f32 [S,3,3,3], RTs f64 [S,3,4,4])."""
+    def submit(self, Ks: np.ndarray, RTs: np.ndarray) -> int:
+        """Start computing F/P of one batch (Ks f32 [S,3,3,3], RTs f64 [S,3,4,4]);
+        returns the job's ticket."""
+        with self._lock:
+            return self._submit(Ks, RTs)
+
+    def _submit(self, Ks, RTs) -> int:
+        if not self.procs:
+            raise RuntimeError("RigWorkers: closed")
         if self.pending is not None:
             raise RuntimeError("RigWorkers: collect the previous result first")
         Ks = np.asarray(Ks, dtype=np.float32)
@@ -162,13 +176,22 @@ class RigWorkers:
         for w in range(n):
             i0, i1 = S * w // n, S * (w + 1) // n
             self._send(w, f"job {slot.shm_in.name} {slot.shm_out.name} {slot.S} {i0} {i1}")
-        self.pending = (k, S, n)
+        ticket = next(self._tickets)
+        self.pending = (ticket, k, S, n)
+        return ticket
 
-    def result(self) -> Tuple[np.ndarray, np.ndarray]:
-        """-> (F f64 [S*3, 9], P f64 [S, 3, 3, 4]) of the submitted batch (copies)."""
+    def result(self, ticket: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """-> (F f64 [S*3, 9], P f64 [S, 3, 3, 4]) of the submitted batch (copies).
+        ``ticket`` (what ``submit`` returned), if given, must be the job in flight."""
+        with self._lock:
+            return self._result(ticket)
+
+    def _result(self, ticket):
         if self.pending is None:
             raise RuntimeError("RigWorkers: nothing submitted")
-        k, S, n = self.pending
+        tk, k, S, n = self.pending
+        if ticket is not None and ticket != tk:
+            raise RuntimeError(f"RigWorkers: job {ticket} is not the one in flight ({tk})")
         self.pending = None
         replies = [self.procs[w].stdout.readline().strip() for w in range(n)]
         bad = [r for r in replies if r != "ok"]
@@ -180,12 +203,18 @@ class RigWorkers:
         del F, P
         return out
 
+    def drain(self) -> None:
+        """Collect and drop the job in flight, if any (a consumer that stopped
+        early leaves the pool ready for the next submit)."""
+        with self._lock:
+            if self.pending is not None:
+                try:
+                    self._result(None)
+                except RuntimeError:
+                    pass
+
     def close(self) -> None:
-        if self.pending is not None:
-            try:
-                self.result()
-            except RuntimeError:
-                pass
+        self.drain()
         for p in self.procs:
             try:
                 p.stdin.close()

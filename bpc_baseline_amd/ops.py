@@ -326,16 +326,18 @@ class PairwisePlan:
 
     ``row_align``: rows of matrix (s, p) are ``ld = roundup(n_b, row_align)``
     floats apart (include/mvmatch.h, mvm_pairwise_residual_argmin_pitched).
-    "auto" (the default) pitches rows to 128-byte lines (32 floats) when some
-    view's count is not a multiple of 32 -- the ragged views real detectors
-    produce, whose unpitched rows would start mid-line -- and keeps the
+    1 (the default) is the unpitched layout: matrices back to back, rows of
+    n_b floats.  "auto" (what the bench and the batch paths ask for) pitches
+    rows to 128-byte lines (32 floats) when some view's count is not a
+    multiple of 32 -- the ragged views real detectors produce, whose unpitched
+    rows would start mid-line, ~1.4x slower per byte -- and keeps the
     unpitched layout otherwise (then the two are the same).  ``matrix()``
     returns the (n_a, n_b) view of a matrix either way; ``compact()`` the
     unpitched flat layout.
     """
 
     def __init__(self, cam_offs: np.ndarray, n_scenes: int, n_cams: int, pairs,
-                 device: torch.device | str = "cuda", row_align="auto"):
+                 device: torch.device | str = "cuda", row_align=1):
         cam_offs = np.asarray(cam_offs, dtype=np.int64)
         pairs = np.asarray(pairs, dtype=np.int32).reshape(-1, 2)
         counts = np.diff(cam_offs).reshape(n_scenes, n_cams)

@@ -106,7 +106,9 @@ def test_bench_rccl_process_group_single_rank(tmp_path):
                        env=env, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["gather_check"] == "rank-0 rows equal after gather"
+    rows = line["parity_rows_detail"]["rows_checked"]
+    assert rows == 40 * 6 * 1024
+    assert line["parity_rows"] == f"{rows}/{rows} bit-exact vs oracle"
     assert line["parity"].startswith("bit-exact")
     assert "nccl" in line["config"]["parallelism"]
 
@@ -154,7 +156,10 @@ def test_ranks_real_kernel_equal_single_process(tmp_path, world, n_scenes):
     assert multi["process_group"]["world_size"] == world
     assert multi["process_group"]["backend"] == "gloo"
     assert multi["config"]["n_scenes_total"] == n_scenes
-    assert multi["gather_check"] == "rank-0 rows equal after gather"
+    rows = n_scenes * 6 * 1024
+    for line in (single, multi):     # every rank's rows, as gathered to rank 0
+        assert line["parity_rows"] == f"{rows}/{rows} bit-exact vs oracle"
+    assert multi["parity_rows_detail"]["ranks"] == world
     assert multi["parity"].startswith("bit-exact") and single["parity"].startswith("bit-exact")
     assert multi["step_split"]["gather_ms"] > 0
     # the N > 1 line carries what the N = 1 line does, measured the same way:
@@ -213,3 +218,84 @@ def test_bench_graph_replay_single_gpu(tmp_path, workload, mode):
     w = line["roofline"]["dispatch_window"]
     # warmup step (3) + the untimed first replay (2 steps x 3) | 2 x 3 timed | PCIe leg (3)
     assert (w["before"], w["timed"], w["after"]) == (3 + 6, 6, 3)
+
+
+def _bench_env():
+    env = dict(os.environ)
+    for k in ("MVM_DIST_FORCE", "MVM_DIST_BACKEND", "WORLD_SIZE", "RANK", "LOCAL_RANK",
+              "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_launches_its_own_ranks(tmp_path, world):
+    """`python bench.py --gpus N` with no launcher starts N ranks itself (torchrun
+    as a child process) and every rank joins one process group of N."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(world), "--dry-run"],
+                       env=_bench_env(), capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == world
+    assert line["process_group"] == {"world_size": world, "backend": "gloo"}
+    assert line["ranks_seen"] == list(range(world))
+    assert f"launching {world} ranks" in r.stderr
+
+
+@pytest.mark.parametrize("env_world,gpus", [("3", 2), ("1", 2), ("2", 1)])
+def test_bench_world_mismatch_fails(env_world, gpus):
+    """A process group whose size is not --gpus ends the run non-zero (never
+    a line with another n_gpus than asked for)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(_bench_env(), WORLD_SIZE=env_world, RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(gpus), "--dry-run"],
+                       env=env, capture_output=True, text=True, timeout=120, cwd=repo)
+    assert r.returncode != 0
+    assert f"--gpus {gpus} but WORLD_SIZE={env_world}" in r.stderr
+    assert not r.stdout.strip()
+
+
+def test_init_timeout_reaches_process_group(tmp_path):
+    """init_from_env gives the process group a finite collective timeout."""
+    mp.spawn(_timeout_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert float((tmp_path / "timeout").read_text()) == 7.0
+
+
+def _timeout_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bpc_baseline_amd.distributed import init_from_env
+    env = init_from_env(backend="gloo", use_gpu=False, timeout_s=7)
+    if env.is_root:
+        with open(os.path.join(out_dir, "timeout"), "w") as fh:
+            fh.write(str(env.timeout.total_seconds()))
+    env.barrier()
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2])
+def test_bench_gpus_n_without_launcher(tmp_path, world):
+    """`MVM_DIST_BACKEND=gloo python bench.py --gpus 2` with no launcher prefix:
+    bench.py starts the ranks itself, the line says n_gpus 2 with a process
+    group of 2, and every gathered association row is bit-exact vs the oracle."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(_bench_env(), MVM_DIST_BACKEND="gloo")
+    n_scenes = 24
+    line = _run_bench(repo, [sys.executable, "bench.py", "--gpus", str(world), "--scenes",
+                             str(n_scenes), "--chunk", "8", "--steps", "1", "--warmup", "1",
+                             "--cpu-seconds", "0"], env, tmp_path, "nolauncher")
+    assert line["n_gpus"] == world
+    assert line["process_group"]["world_size"] == world
+    rows = n_scenes * 6 * 1024
+    assert line["parity_rows"] == f"{rows}/{rows} bit-exact vs oracle"
+    assert line["roofline"]["per_slot"]["slots"]

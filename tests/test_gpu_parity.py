@@ -28,8 +28,22 @@ def run_pairwise(dev, pts, cam_offs, F, pairs, S, C, want_dist=True, options=Non
         options=options or None)
     torch.cuda.synchronize()
     if want_dist:
+        if plan.dist_size != plan.n_dist:
+            assert_padding_inf(plan, d.cpu().numpy())
         d = plan.compact(d)
     return d.cpu().numpy(), a.cpu().numpy(), m.cpu().numpy()
+
+
+def assert_padding_inf(plan, h):
+    """include/mvmatch.h: every kernel path writes +inf into a pitched row's
+    padding columns (degenerate and non-finite rows, the generic and strided
+    paths, multi-tile views included)."""
+    for sp in range(plan.na.size):
+        o, na, nb, ld = (int(x) for x in (plan.dist_offs_host[sp], plan.na[sp], plan.nb[sp],
+                                           plan.ld[sp]))
+        pad = h[o:o + na * ld].reshape(na, ld)[:, nb:]
+        assert np.all(np.isposinf(pad)), \
+            f"matrix {sp} ({na}x{nb}, ld {ld}): padding not +inf at {np.argwhere(~np.isposinf(pad))[:4]}"
 
 
 def run_cube(dev, pts, cam_offs, F, S, options=None):

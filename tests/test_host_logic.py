@@ -50,8 +50,13 @@ def test_pairwise_plan_pitched_rows(row_align):
         assert np.array_equal(got, flat[o:o + na * nb].reshape(na, nb))
         o += na * nb
     assert np.array_equal(plan.compact(torch.from_numpy(pitched)).numpy(), flat)
-    u = ops.PairwisePlan(np.array([0, 64, 96], np.int64), 1, 2, [[0, 1]], device="cpu")
+    u = ops.PairwisePlan(np.array([0, 64, 96], np.int64), 1, 2, [[0, 1]], device="cpu",
+                         row_align="auto")
     assert u.row_align == 1 and u.dist_size == u.n_dist == 64 * 32
+    # the default is the unpitched contract (matrices back to back) even for
+    # ragged counts: pitching is opt-in
+    d = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu")
+    assert d.row_align == 1 and d.dist_size == d.n_dist
     with pytest.raises(ValueError):
         ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device="cpu", row_align=48)
 
@@ -448,6 +453,7 @@ def test_bench_rejects_fewer_scenes_than_ranks(monkeypatch):
         device = "cpu"
 
     monkeypatch.setattr(bench, "init_from_env", lambda: Env())
+    monkeypatch.setenv("WORLD_SIZE", "8")      # as a rank of an 8-rank launch
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8", "--scenes", "4"])
     with pytest.raises(SystemExit, match="every rank needs at least one scene"):
         bench.main()
@@ -534,3 +540,65 @@ def test_lsap_slot_capacity_covers_every_shape():
         cap = max(plan(min(rcap, ccap), ccap), plan(rcap, min(ccap, rcap - 1)) if rcap > 1 else 0)
         worst = max(plan(r, c) for r in range(1, rcap + 1) for c in range(1, ccap + 1))
         assert worst <= cap, (rcap, ccap, worst, cap)
+
+
+def test_rig_workers_tickets_and_drain():
+    """A result() with another job's ticket raises; drain() collects a job in
+    flight so the pool takes the next submit."""
+    from bpc_baseline_amd.synth import make_rig
+    from bpc_baseline_amd.inference.rig_workers import RigWorkers
+    from bpc_baseline_amd.inference.utils.camera_utils import rig_matrices
+    rng = np.random.default_rng(3)
+    Ks, RTs = make_rig(rng, 3)
+    Ks = np.stack([np.stack(Ks)] * 4).astype(np.float32)
+    RTs = np.stack([np.stack(RTs)] * 4)
+    with RigWorkers(2) as rw:
+        t1 = rw.submit(Ks, RTs)
+        with pytest.raises(RuntimeError, match="collect the previous result first"):
+            rw.submit(Ks, RTs)
+        with pytest.raises(RuntimeError, match="not the one in flight"):
+            rw.result(t1 + 1)
+        rw.drain()                                  # the abandoned job
+        t2 = rw.submit(Ks, RTs)
+        F, P = rw.result(t2)
+        Fr, _ = rig_matrices(Ks, RTs)
+        assert np.array_equal(F.view(np.int64), Fr.view(np.int64))
+        rw.drain()                                  # nothing in flight: no-op
+
+
+def test_capture_stream_abandoned_then_reused(monkeypatch):
+    """A consumer that breaks out of match_capture_stream leaves the next
+    batch's F/P job in flight; the stream collects it, so a second stream on
+    the same thread's pool runs (batch_match.py:204).  Threads get
+    their own pools.  match_captures is replaced by a host stand-in that
+    returns the F it was given (the device chain is covered by -m gpu)."""
+    import threading
+    import torch
+    from bpc_baseline_amd.inference import batch_match as bm
+    from bpc_baseline_amd.synth import make_rig
+    from bpc_baseline_amd.inference.utils.camera_utils import rig_matrices
+    monkeypatch.setattr(bm, "match_captures", lambda *a, F=None, proj=None, **k: F)
+    rng = np.random.default_rng(9)
+
+    def batch(S):
+        rigs = [make_rig(rng, 3) for _ in range(S)]
+        Ks = np.stack([np.stack(r[0]) for r in rigs]).astype(np.float32)
+        RTs = np.stack([np.stack(r[1]) for r in rigs])
+        return (torch.zeros(1), None, None, torch.zeros(3 * S + 1, dtype=torch.int64), Ks, RTs)
+
+    batches = [batch(5), batch(6), batch(7)]
+    for F in bm.match_capture_stream(batches, rig_workers=2):
+        break                                       # batch 1's job is in flight here
+    got = list(bm.match_capture_stream(batches, rig_workers=2))
+    for b, F in zip(batches, got):
+        assert np.array_equal(F.numpy().view(np.int64), rig_matrices(b[4], b[5])[0].view(np.int64))
+    with pytest.raises(ZeroDivisionError):
+        for F in bm.match_capture_stream(batches, rig_workers=2):
+            1 / 0                                   # an exception in the consumer
+    assert len(list(bm.match_capture_stream(batches, rig_workers=2))) == 3
+    pools = []
+    th = threading.Thread(target=lambda: pools.append(bm.rig_worker_pool(2)))
+    th.start()
+    th.join()
+    assert pools[0] is not bm.rig_worker_pool(2)
+    pools[0].close()

@@ -120,7 +120,7 @@ if args.workload == "cube":
 else:
     b = (make_scenes(args.scenes or 1000, 3, 256, seed=0) if args.workload == "c2"
          else make_scenes(args.scenes or 1000, 4, 1024, seed=0))
-    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev, row_align="auto")
     n_out = plan.dist_size
     pa = (ctypes.c_int32 * len(plan.pair_a))(*plan.pair_a)
     pb = (ctypes.c_int32 * len(plan.pair_b))(*plan.pair_b)

@@ -35,7 +35,7 @@ if args.workload == "cube":
 else:
     b = (make_scenes(1000, 3, 256, seed=0) if args.workload == "c2"
          else make_scenes(1000, 4, 1024, seed=0))
-    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev, row_align="auto")
     n_out = plan.dist_size
 pts, co, F = (torch.from_numpy(x).to(dev) for x in (b.pts, b.cam_offs, b.F))
 out = torch.empty(n_out, dtype=torch.float32, device=dev)

@@ -45,7 +45,7 @@ rows = []
 for n in sizes:
     C, P = b.n_cams, b.n_pairs
     co = b.cam_offs[:n * C + 1]
-    plan = ops.PairwisePlan(co, n, C, b.pairs, device=dev)
+    plan = ops.PairwisePlan(co, n, C, b.pairs, device=dev, row_align="auto")
     pts = torch.from_numpy(b.pts[:int(co[-1])]).to(dev)
     cot = torch.from_numpy(co).to(dev)
     F = torch.from_numpy(b.F[:n * P]).to(dev)

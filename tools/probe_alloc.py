@@ -38,7 +38,7 @@ if args.cube:
     plan.n_dist = plan.n_cube
 else:
     b = make_scenes(args.scenes, 4, 1024, seed=0)
-    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
+    plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev, row_align="auto")
 pts, co, F = (torch.from_numpy(x).to(dev) for x in (b.pts, b.cam_offs, b.F))
 am = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
 mv = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)

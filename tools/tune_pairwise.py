@@ -47,7 +47,7 @@ args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 b = make_scenes(args.scenes, args.cams, args.dets, seed=0)
-plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev)
+plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev, row_align="auto")
 pts = torch.from_numpy(b.pts).to(dev)
 co = torch.from_numpy(b.cam_offs).to(dev)
 F = torch.from_numpy(b.F).to(dev)
