@@ -122,8 +122,8 @@ __device__ __forceinline__ void row_fast_strided(const ColRegs &c, double rl0, d
 
 // Generic row: degenerate lines (9999 sentinel), non-finite or huge values,
 // tails, unaligned rows, no output buffer.  Column of slot q: jbase + q*jstep.
-// Columns past the view but inside the row's pitch (j < lim) are stored too:
-// their pad lines give +inf, as the other paths write.
+// Columns past the view but inside the row's pitch (j < lim) are stored too,
+// as +inf, which is what the other paths write there.
 template <bool ARGMIN, typename OutT>
 __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl1, double rl2,
                                          double rx, double ry, bool rdeg, OutT *drow, int jbase,
@@ -133,8 +133,10 @@ __device__ __forceinline__ void row_safe(const ColRegs &c, double rl0, double rl
         double d1 = line_dist(c.l0[q], c.l1[q], c.l2[q], rx, ry);
         d1 = (c.state[q] == kDeg) ? kSentinel : d1;
         const double d2 = rdeg ? kSentinel : line_dist(rl0, rl1, rl2, c.x[q], c.y[q]);
-        const double e = 0.5 * (d1 + d2);                                            // :28
         const bool valid = c.state[q] != kNone;
+        // :28; a pitched row's padding is +inf whatever the row holds (a NaN
+        // row point would otherwise make the pad line's value NaN)
+        const double e = valid ? 0.5 * (d1 + d2) : __builtin_inf();
         const int j = jbase + q * jstep;
         // j < lim: the view's columns and a pitched row's padding (lim = ld >= n_b)
         if (drow && j < lim) drow[j] = (OutT)e;   // default policy: L2 merges partial lines
@@ -315,7 +317,14 @@ __device__ __forceinline__ void load_col_lines(const double *pts, const double (
         if (j < nb) {
             x = pts[2 * (ob + j)];
             y = pts[2 * (ob + j) + 1];
+#ifdef MVM_DIAG_CHEAP_LINES   // diagnostic build only (phase timing): unnormalised lines
+            l0 = f[0] * x;
+            l1 = f[4] * y;
+            l2 = f[8];
+            st = kOk;
+#else
             st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
+#endif
         }
         s_l0[jj] = l0;
         s_l1[jj] = l1;
@@ -346,7 +355,14 @@ __device__ __forceinline__ void put_row_line(double *slot, const double *s_rpt,
     if (valid) {
         x = s_rpt[2 * lrow];
         y = s_rpt[2 * lrow + 1];
+#ifdef MVM_DIAG_CHEAP_LINES   // diagnostic build only (phase timing): unnormalised lines
+        l0 = f[0] * x;
+        l1 = f[4] * y;
+        l2 = f[8];
+        deg = false;
+#else
         deg = row_line(f, x, y, l0, l1, l2);
+#endif
     }
     slot[0] = l0;
     slot[1] = l1;
@@ -513,6 +529,15 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             // reload drained all of them
             int lz = lane;
             __asm__ volatile("" : "+v"(lz));
+#ifdef MVM_DIAG_NO_ASSOC   // diagnostic build only (phase timing): no group reduction
+            {
+                uint32_t x = 0;
+#pragma unroll
+                for (int r = 0; r < RPW; ++r) x ^= bbits[r];
+                if (lz < RPW && args.minval) args.minval[g.row_off0 + grow0 + lz * RST] = __uint_as_float(x);
+                continue;
+            }
+#endif
             uint32_t k;
             int w;
             bool tie;

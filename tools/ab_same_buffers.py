@@ -31,6 +31,9 @@ ap.add_argument("--opts", default="default",
 ap.add_argument("--workload", choices=["cube", "c3", "c2"], default="cube")
 ap.add_argument("--buffers", type=int, default=6)
 ap.add_argument("--rounds", type=int, default=3)
+ap.add_argument("--no-check", action="store_true",
+                help="skip the bit-equality check across builds (diagnostic builds, e.g. "
+                     "MVM_DIAG_CHEAP_LINES / MVM_DIAG_NO_ASSOC, compute other values)")
 ap.add_argument("--scenes", type=int, default=None, help="scenes per launch (cube 250, c3 1000)")
 ap.add_argument("--dets", type=int, default=256, help="detections per view (cube)")
 ap.add_argument("--alloc", default=None,
@@ -170,7 +173,7 @@ for rnd in range(args.rounds + 1):
             torch.cuda.synchronize()
             if rnd:
                 times[(name, i)].append(e0.elapsed_time(e1) / reps)
-            if rnd == 0:   # every build's results equal the first's on this buffer
+            if rnd == 0 and not args.no_check:   # every build's results equal the first's
                 chk = (am.cpu().numpy().tobytes(), out[:1 << 22].cpu().numpy().tobytes(),
                        out[-(1 << 22):].cpu().numpy().tobytes())
                 if ref is None:
