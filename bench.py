@@ -601,16 +601,24 @@ def main():
         launch(chunks[k])
         return last_slot[id(chunks[k])]
 
+    # every event of the timed steps is created up front: creating two per
+    # launch inside the loop cost the host ~30 us per C2 step, longer than the
+    # GPU took for some launches, so the GPU waited on the host between them
+    def new_event():
+        return torch.cuda.Event(enable_timing=True)
+    step_events = [[(new_event(), new_event()) for _ in chunks] for _ in range(args.steps)]
+    tail_events = [(new_event(), new_event()) for _ in range(args.steps)]
+
     def timed_step(s, events, tails):
         for k, c in enumerate(chunks):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0, e1 = step_events[s][k]
             e0.record(stream)
             slot = run_launch(s, k)
             e1.record(stream)
             events.append((e0, e1, c.nbytes, c.units, 1, slot))
             if overlap:
                 gatherer.issue(k)
-        ec, es = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ec, es = tail_events[s]
         ec.record(stream)     # the step's compute is done here ...
         res = gatherer.finish() if overlap else gather_rows(env, argmin, minval)
         es.record(stream)     # ... and its association is on rank 0 here: the exposed tail
