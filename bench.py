@@ -19,10 +19,16 @@ launches of at most ``--chunk`` scenes, at least ``--min-launches`` per rank
 (5 with N > 1: the gather piece of launch k overlaps launch k+1, so only the
 last piece is exposed, and that last launch is a short one, ~1/4 of the
 others); every residual is stored to HBM.  At every N each
-launch of each timed step is a hipGraph captured outside the timed region and
-replayed in order, with N > 1 followed by its gather piece, so the 1 -> N
-curve compares the same launch path (``--graph steps``: one graph for all K
-steps, one GPU only; ``--graph off``: eager op calls).
+launch of each timed step of C3 is a hipGraph captured outside the timed
+region and replayed in order, with N > 1 followed by its gather piece, so the
+1 -> N curve compares the same launch path (``--graph steps``, the default
+for C2 on one GPU: one graph for all K steps; ``--graph off``: eager op calls).
+
+``python bench.py --gpus N`` (N > 1) run without a launcher starts the N
+ranks itself: torchrun in a child process, this process making no GPU call;
+every rank checks that the process group it joined has N ranks.  After the
+timed region every association row of the last step -- all ranks' rows, as
+gathered to rank 0 -- is compared with the CPU oracle (``parity_rows``).
 By default every launch of the timed steps writes its own output allocation
 as far as HBM holds them (C3: ten 25 GB buffers, 252 GB, one per launch of a
 step; C2: one per step), taken round robin, so a step's outputs all stay
@@ -415,8 +421,10 @@ def main():
     ap.add_argument("--output", choices=["resident", "ring"], default="resident",
                     help="resident (default): one output allocation per launch of the timed "
                          "steps as far as HBM holds them (reused round robin); ring: one")
-    ap.add_argument("--graph", choices=["launch", "steps", "off"], default="launch",
-                    help="launch (default, every N): each launch of each timed step is a hipGraph "
+    ap.add_argument("--graph", choices=["auto", "launch", "steps", "off"], default="auto",
+                    help="auto (default): steps for the c2 workload on one GPU (its 0.14 ms "
+                         "launches are shorter than the host's per-replay cost), launch "
+                         "otherwise; launch: each launch of each timed step is a hipGraph "
                          "captured outside the timed region and replayed in order, the gather "
                          "piece of launch k issued right after its replay; steps: one hipGraph "
                          "holding all K steps (one GPU only: a step with N > 1 has collectives); "
@@ -469,6 +477,13 @@ def main():
     if env.backend == "nccl" and torch.cuda.device_count() < world:
         raise SystemExit(f"error: {world} RCCL ranks but {torch.cuda.device_count()} visible GPU(s)")
     dev = env.device
+    if args.graph == "auto":
+        # per-launch replays (and the per-launch HIP events around them) cost the
+        # host ~15 us per replay; a 0.14 ms C2 launch cannot hide that, C3's
+        # 4 ms launches do.  Events recorded inside a captured graph cannot be
+        # timed on ROCm (tools/probes/graph_events.py), so "steps" times the K
+        # steps with one event pair.
+        args.graph = "steps" if (args.workload == "c2" and not env.initialised) else "launch"
     if args.graph == "steps" and env.initialised:
         raise SystemExit("--graph steps needs a single GPU without a process group "
                          "(the step's gather is a collective)")
