@@ -175,7 +175,12 @@ __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, doub
                                               double rx, double ry, float *drow, int jbase,
                                               uint32_t &bbits, bool st = true) {
     float v[kColsPerLane];
+#ifdef MVM_DIAG_NO_ARITH   // diagnostic build only (phase timing): the stores without the pair arithmetic
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)(rx + c.x[q]);
+#else
     pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
+#endif
     if (STORE && (!MASKED || st)) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
     bbits = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2])),
                      __float_as_uint(v[3]), bbits);
