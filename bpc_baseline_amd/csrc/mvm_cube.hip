@@ -177,10 +177,17 @@ __device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q
 // policy lets L2 merge them (nontemporal partial lines reach HBM as masked
 // writes: 200^3 1.91 -> 1.57 ms, 100^3 1.11 -> 1.06 ms per launch on the same
 // buffers, profiles/r03/ab/cube_partial_lines_*.log).  Uniform per launch.
-__device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[4],
+template <int KPL = kColsPerLane>
+__device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[KPL],
                                                bool lined) {
-    if (lined) store4_nt_row<1>(base, off, v);
-    else store4_nt_row<0>(base, off, v);
+    static_assert(KPL == 3 || KPL == 4, "3 or 4 k per lane");
+    if constexpr (KPL == 4) {
+        if (lined) store4_nt_row<1>(base, off, v);
+        else store4_nt_row<0>(base, off, v);
+    } else {
+        if (lined) store3_row<1>(base, off, v);
+        else store3_row<0>(base, off, v);
+    }
 }
 
 // A scene whose third view is empty (P == 0) has no cube entries, but its
@@ -406,10 +413,14 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // whole wave, which cost more than the row-steps themselves at P <= 64
 // (same buffers: 48^3 2.96 -> 2.26 ms, 64^3 1.92 -> 1.56 ms per 8 GB launch,
 // profiles/r03/ab/cube_group_argmin_*.log).
-template <int kCubeIB, int kCubeRPW, int SPLIT = 1>
+// KPL: k per lane.  3 where the view fits 3 * (64 / SPLIT) k (48 / 96 / 192):
+// a quarter fewer VALU per row step than 4 k per lane, whose last quarter of
+// lanes would hold no k there; rows are stored with `global_store_dwordx3`.
+template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane>
 __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr bool HALF = SPLIT > 1;   // split mapping
     static_assert(SPLIT == 1 || (kCubeRPW == 8 && (SPLIT == 2 || SPLIT == 4)), "8 rows in 2 or 4 groups");
+    static_assert(KPL == 3 || KPL == kColsPerLane, "3 or 4 k per lane");
     constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
     constexpr int kLPR = kWave / SPLIT;           // lanes per row
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
@@ -453,12 +464,14 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
     const int hl = lane / kLPR;                                      // row group of the lane
-    const int kb = kColsPerLane * (lane % kLPR);
+    const int kb = KPL * (lane % kLPR);
     const int kvalid = P - kb;
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
-    // vector rows: every lane's 4 k valid or none (P % 4 == 0), 16-byte aligned
-    const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+    // vector rows: every lane's KPL k valid or none (P % KPL == 0); 16-byte
+    // aligned for 4 k per lane (dwordx3 stores need 4 bytes)
+    const bool full = (KPL == 4 ? ((P & 3) == 0) && ((coff & 3) == 0) : (P % KPL) == 0) &&
+                      args.cube;
     const bool act_k = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
@@ -542,9 +555,9 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     };
     // ---- prologue 2: the wave's e23 rows into registers ---------------------
     bool tame_in = true;   // every residual this thread produced is <= kTameResidual
-    double a23[kLaneRows][kColsPerLane];
+    double a23[kLaneRows][KPL];
 #pragma unroll
-    for (int q = 0; q < kColsPerLane; ++q) {
+    for (int q = 0; q < KPL; ++q) {
         const ColRec cl = s_c23[min(kb + q, kChunk - 1)];
 #pragma unroll
         for (int r = 0; r < kLaneRows; ++r) {
@@ -586,11 +599,14 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
         constexpr bool FAST = decltype(fast_tag)::value;
         for (int ii = 0; ii < ni; ++ii) {
             const int i = ib + i_stride * ii;
-            double a13[kColsPerLane];
-            {
+            double a13[KPL];
+            if constexpr (KPL == 4) {
                 const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
                 const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
                 a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+            } else {
+#pragma unroll
+                for (int q = 0; q < KPL; ++q) a13[q] = s13[ii][min(kb + q, kChunk - 1)];
             }
             uint32_t key[kLaneRows];
             int32_t idx[kLaneRows];
@@ -602,41 +618,41 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
                 const int rr = r + hl * kLaneRows;                 // the wave row
                 const bool act = act_k && rr < nrows;              // HALF: the upper row may not exist
                 const double v12 = s12[ii][wave * kCubeRPW + rr];
-                double sum[kColsPerLane], q0[kColsPerLane];
+                double sum[KPL], q0[KPL];
                 bool ok = true;
 #pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
+                for (int q = 0; q < KPL; ++q) {
                     sum[q] = (v12 + a13[q]) + a23[r][q];          // (e12 + e13) + e23, :81
                     q0[q] = third_q(sum[q]);
                     if (!FAST) ok &= third_ok(q0[q]);
                 }
-                float v[kColsPerLane];
+                float v[KPL];
                 const int64_t row = (int64_t)i * M + j0 + rr;
                 if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                    for (int q = 0; q < KPL; ++q) v[q] = (float)q0[q];
                     if (act) {
-                        cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                      (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
+                        cube_row_store<KPL>(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                            (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
                     }
                     Best b{v[0], kb};
 #pragma unroll
-                    for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                    for (int q = 1; q < KPL; ++q) best_update_fast(b, v[q], kb + q);
                     key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
                     idx[r] = act ? b.j : 0x7FFFFFFF;
                 } else {
                     Best b{__uint_as_float(0x7F800000u), 0x7FFFFFFF};
                     // the IEEE division only when some lane needs it (uniform branch)
-                    double qq[kColsPerLane];
+                    double qq[KPL];
 #pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) qq[q] = q0[q];
+                    for (int q = 0; q < KPL; ++q) qq[q] = q0[q];
                     if (!__all(ok || !act)) {
 #pragma unroll
-                        for (int q = 0; q < kColsPerLane; ++q)
+                        for (int q = 0; q < KPL; ++q)
                             qq[q] = third_ok(q0[q]) ? q0[q] : sum[q] / 3.0;
                     }
 #pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) {
+                    for (int q = 0; q < KPL; ++q) {
                         v[q] = (float)qq[q];
                         if (act && q < kvalid) {
                             if (args.cube)
@@ -706,7 +722,7 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
     // in-lane argmin from unsigned minima of the float32 bits (the values are
     // finite and non-negative here, so they order like their bits) -- the
     // first q holding the minimum is np.argmin's first index within the lane.
-    auto full_loop = [&]() {
+    auto full_loop = [&](auto) {   // generic: instantiated only where called (4 k per lane)
         constexpr uint64_t kRowBytes = kChunk * sizeof(float);
         uint64_t rp = reinterpret_cast<uint64_t>(args.cube + coff) +
                       (uint64_t)((int64_t)ib * M + j0) * kRowBytes;
@@ -760,9 +776,9 @@ __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused
             rp += i_step;
         }
     };
-    if constexpr (SPLIT == 1) {
+    if constexpr (SPLIT == 1 && KPL == kColsPerLane) {
         if (tile_fast && nrows == kCubeRPW && P == kChunk) {   // uniform
-            full_loop();
+            full_loop(0);
             return;
         }
     }
@@ -1264,6 +1280,9 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
         o.cube_rows_per_instr != 4)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_rows_per_instr %d not 0, 1, 2 or 4",
                         (int)o.cube_rows_per_instr);
+    if (o.cube_cols_per_lane != 0 && o.cube_cols_per_lane != 3 && o.cube_cols_per_lane != 4)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d not 0, 3 or 4",
+                        (int)o.cube_cols_per_lane);
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
     if (!pts_dev || !cam_offs_dev || !F_dev || !row_offs_dev)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
@@ -1318,14 +1337,26 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
             return mvm_check_launch("triplet_fused_chunked_kernel");
         }
         // tiles of 16 i x 32 j; views of <= 64 / <= 128 put four / two (i, j)
-        // rows in every wave instruction
+        // rows in every wave instruction; 3 k per lane where the view fits
+        // them (<= 48 / 96 / 192 at four / two / one rows per instruction)
         const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
-        if (want >= 4 && max_n <= kChunk / 4)
-            triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
-        else if (want >= 2 && max_n <= kChunk / 2)
-            triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
-        else
-            triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c);
+        const int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
+        const int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane
+                                             : (max_n <= 3 * (kWave / split) ? 3 : 4);
+        if (kpl == 3 && max_n > 3 * (kWave / split))
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
+                            "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
+                            (int)max_n, 3 * (kWave / split));
+        if (split == 4) {
+            if (kpl == 3) triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c);
+            else triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
+        } else if (split == 2) {
+            if (kpl == 3) triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c);
+            else triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
+        } else {
+            if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3><<<grid, block, 0, s>>>(c);
+            else triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c);
+        }
         return mvm_check_launch("triplet_fused_kernel");
     }
     // workspace forms: the fp64 pair matrices e12, e13, e23 of every scene

@@ -160,6 +160,18 @@ __device__ __forceinline__ void store4_nt_row(uint64_t row_base, uint32_t byte_o
     else
         *reinterpret_cast<g_f32x4 *>(row_base + byte_off) = v;
 }
+// 3 consecutive outputs of one lane (rows of 3-k lanes): `global_store_dwordx3`,
+// saddr form, 4-byte aligned
+typedef float f32x3 __attribute__((ext_vector_type(3)));
+typedef f32x3 __attribute__((address_space(1), aligned(4))) g_f32x3;
+template <int NT = 1>
+__device__ __forceinline__ void store3_row(uint64_t row_base, uint32_t byte_off, const float v3[3]) {
+    const f32x3 v = {v3[0], v3[1], v3[2]};
+    if constexpr (NT == 1)
+        __builtin_nontemporal_store(v, reinterpret_cast<g_f32x3 *>(row_base + byte_off));
+    else
+        *reinterpret_cast<g_f32x3 *>(row_base + byte_off) = v;
+}
 __device__ __forceinline__ void store4_nt(double *dst, const double e[4]) {
     const f64x2 lo = {e[0], e[1]}, hi = {e[2], e[3]};
     __builtin_nontemporal_store(lo, reinterpret_cast<f64x2 *>(dst));

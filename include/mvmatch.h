@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 3
+#define MVM_ABI_VERSION 4
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -123,6 +123,10 @@ typedef struct mvm_options {
                                        the workgroup's 4 waves (at each row step they
                                        store 4 adjacent rows); -1 each wave's rows
                                        contiguous (ABI 3) */
+    int32_t cube_cols_per_lane;     /* FUSED (views <= 256): 0 default (3 where the view
+                                       fits 3 k per lane: <= 48 / 96 / 192 at four / two /
+                                       one rows per instruction, else 4); 3 or 4 (ABI 4;
+                                       3 on a view that does not fit is an error) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

@@ -139,6 +139,15 @@ def test_options_init_and_validation(lib):
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(bad), None)
     assert st == 1 and b"cube_kernel" in lib.mvm_last_error_string()
+    bad = _native.make_options(cube_cols_per_lane=5)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(bad), None)
+    assert st == 1 and b"cube_cols_per_lane" in lib.mvm_last_error_string()
+    # 3 k per lane forced on a view wider than 3 x 64 at one row per instruction
+    bad = _native.make_options(cube_kernel="fused", cube_rows_per_instr=1, cube_cols_per_lane=3)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 200, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(bad), None)
+    assert st == 1 and b"exceed 192" in lib.mvm_last_error_string()
     o.size = 3                                      # not a struct size
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(o), None)

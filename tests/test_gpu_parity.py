@@ -281,18 +281,22 @@ def test_pairwise_argmin_only(cuda, argmin_path):
 
 
 # --------------------------------------------------------------- cube ----
-@pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "workspace",
-                        "generic"])
+@pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "fused_kpl4",
+                        "fused_rows1_kpl4", "workspace", "generic"])
 def cube_path(request):
     """mvm_options of each cube kernel: the small-scene kernel (views of < 64
     detections), the fused tiled kernel (pair residuals computed in the
     prologue; up to 256, then its k-chunked form) with four / two / one
-    (i, j) rows per wave instruction, the tiled kernel over the fp64
+    (i, j) rows per wave instruction -- 3 k per lane where the view fits them
+    (the default), or 4 forced (kpl4) -- the tiled kernel over the fp64
     workspace (beyond 256: the generic kernel) and the generic kernel."""
     return request.param, {"default": {}, "small": {"cube_kernel": "small"},
                            "fused": {"cube_kernel": "fused"},
                            "fused_rows2": {"cube_kernel": "fused", "cube_rows_per_instr": 2},
                            "fused_rows1": {"cube_kernel": "fused", "cube_rows_per_instr": 1},
+                           "fused_kpl4": {"cube_kernel": "fused", "cube_cols_per_lane": 4},
+                           "fused_rows1_kpl4": {"cube_kernel": "fused", "cube_rows_per_instr": 1,
+                                                "cube_cols_per_lane": 4},
                            "workspace": {"cube_kernel": "workspace"},
                            "generic": {"cube_kernel": "generic"}}[request.param]
 
@@ -328,7 +332,9 @@ def test_cube_golden_batched(cuda, golden, cube_path):
                                         (300, 24, False), (40, 64, True), (7, 1, False),
                                         (2, 512, False), (3, 333, True), (1, 770, False), (2, 200, False),
                                         (2, 384, False), (20, 96, False), (6, 100, True), (5, 128, False),
-                                        (9, 77, True), (4, 68, False)])
+                                        (9, 77, True), (4, 68, False), (3, 160, False),
+                                        (2, 192, False), (3, 48, False), (3, 150, True),
+                                        (4, 190, True), (5, 47, True), (3, 93, False)])
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)

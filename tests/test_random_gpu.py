@@ -117,12 +117,12 @@ def test_pairwise_random_vs_oracle(cuda, seed):
 CUBE_PATHS = [{}, {"cube_kernel": "small"}, {"cube_kernel": "fused"},
               {"cube_kernel": "fused", "cube_rows_per_instr": 2},
               {"cube_kernel": "fused", "cube_rows_per_instr": 1}, {"cube_kernel": "workspace"},
-              {"cube_kernel": "generic"}]
+              {"cube_kernel": "generic"}, {"cube_kernel": "fused", "cube_cols_per_lane": 4}]
 
 
-@pytest.mark.parametrize("seed", range(63))
+@pytest.mark.parametrize("seed", range(64))
 def test_cube_random_vs_oracle(cuda, seed):
-    """Every cube kernel path in turn (seed % 7), the default one included."""
+    """Every cube kernel path in turn (seed % 8), the default one included."""
     import torch
     from bpc_baseline_amd import ops
     rng = np.random.default_rng(9000 + seed)
