@@ -890,6 +890,9 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
     for (int kc = 0; kc < P; kc += kChunk) {
         const int Pc = min(kChunk, P - kc);
         const int kvalid = Pc - kb;
+        // the chunk's column points from a uniform base and 32-bit lane
+        // offsets (saddr loads): no 64-bit per-lane address to keep
+        const double *pk = args.pts + 2 * (c2 + kc);
         if (kc > 0) __syncthreads();   // every wave is done with the previous chunk's s13
         bool tame_in = tame12;
         {   // e13 of this chunk: one column per thread
@@ -897,7 +900,7 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
             double f13[9];
             load_f(F13, f13);
             if (k < Pc) {
-                const double x = args.pts[2 * (c2 + kc + k)], y = args.pts[2 * (c2 + kc + k) + 1];
+                const double x = pk[2 * k], y = pk[2 * k + 1];
                 LineRec cl{0.0, 0.0, 0.0, 0.0};
                 cl.deg = col_line(f13, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
 #pragma unroll 4
@@ -918,8 +921,8 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
             LineRec cl{0.0, 0.0, 0.0, 0.0};
             double x = 0.0, y = 0.0;
             if (q < kvalid) {
-                x = args.pts[2 * (c2 + kc + kb + q)];
-                y = args.pts[2 * (c2 + kc + kb + q) + 1];
+                x = pk[2 * (kb + q)];
+                y = pk[2 * (kb + q) + 1];
                 cl.deg = col_line(f23, x, y, cl.l0, cl.l1, cl.l2) ? 1.0 : 0.0;
             }
 #pragma unroll
@@ -1001,8 +1004,13 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
                         idx[r] = b.j;
                     }
                 }
-                if constexpr (FAST && kCubeRPW == 8 && kWave % 8 == 0) {
-                    // rows x = ii*8 + r land in lanes x % 64 of slot x / 64 directly
+                if constexpr (kCubeRPW == 8 && kWave % 8 == 0) {
+                    // rows x = ii*8 + r land in lanes x % 64 of slot x / 64 directly;
+                    // keys are ordered like np.argmin's rule (NaN 0, no column
+                    // kKeyInvalid) and a lane's columns follow its lane id, so
+                    // the lowest lane holding the minimum has the lowest index
+                    // -- also on the generic chunk path (fewer live registers
+                    // than eight per-row wave reductions)
                     const int x0 = ii * kCubeRPW;   // uniform
                     uint32_t km;
                     int32_t im;
