@@ -20,8 +20,8 @@ pytestmark = pytest.mark.gpu
 
 EDGE_COUNTS = [0, 1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512,
                513, 1000, 1023, 1024, 1025, 1100]
-CUBE_COUNTS = [0, 1, 2, 5, 16, 31, 32, 33, 44, 45, 48, 63, 64, 65, 100, 127, 128, 129, 200, 256,
-               257, 300]
+CUBE_COUNTS = [0, 1, 2, 5, 16, 31, 32, 33, 44, 45, 47, 48, 49, 63, 64, 65, 95, 96, 97, 100, 127,
+               128, 129, 191, 192, 193, 200, 256, 257, 300]
 
 
 def _bits(a):
