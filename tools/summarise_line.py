@@ -11,4 +11,5 @@ print(f"{d['config'].get('launch_mode')} N={d['n_gpus']} value {d['value']:.4g} 
       f"ms/step {d['ms_per_step']:.3f} launch {r['avg_launch_ms']:.4f} ms frac {r['frac']:.4f} "
       f"probe {r.get('write_probe_gbs') or 0:.0f} GB/s of-probe {r.get('frac_of_write_probe') or 0:.3f} "
       f"sclk {d['sclk'].get('mean_mhz', 0):.0f} cpu {cpu.get('value', 0):.3g} "
-      f"tail {sp.get('exposed_tail_ms', 0):.3f} ms | {d['parity']}")
+      f"tail {sp.get('exposed_tail_ms', 0):.3f} ms | {d['parity']} | rows: {d.get('parity_rows')}"
+      + (f" | slots fastest/slowest {r['per_slot']['fastest_over_slowest']:.3f}" if r.get('per_slot') else ""))
