@@ -419,7 +419,9 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane>
 __global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr bool HALF = SPLIT > 1;   // split mapping
-    static_assert(SPLIT == 1 || (kCubeRPW == 8 && (SPLIT == 2 || SPLIT == 4)), "8 rows in 2 or 4 groups");
+    static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)),
+                  "8 or 12 rows in 2 or 4 groups");
+    static_assert(kCubeRPW % SPLIT == 0, "whole rows per lane group");
     static_assert(KPL == 3 || KPL == kColsPerLane, "3 or 4 k per lane");
     constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
     constexpr int kLPR = kWave / SPLIT;           // lanes per row
@@ -1245,7 +1247,7 @@ int grid_check(int64_t blocks) {
 
 CubeFusedArgs fused_args(const double *pts, const int64_t *cam_offs, const double *F,
                          const int64_t *cube_offs, const int64_t *row_offs, float *cube,
-                         int32_t *argmin, float *minval, int max_n, int ib) {
+                         int32_t *argmin, float *minval, int max_n, int ib, int rpw = 8) {
     CubeFusedArgs c{};
     c.pts = pts;
     c.cam_offs = cam_offs;
@@ -1255,7 +1257,7 @@ CubeFusedArgs fused_args(const double *pts, const int64_t *cam_offs, const doubl
     c.cube = cube;
     c.argmin = argmin;
     c.minval = minval;
-    c.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+    c.j_blocks = (max_n + kWaves * rpw - 1) / (kWaves * rpw);
     c.i_blocks = (max_n + ib - 1) / ib;
     return c;
 }
@@ -1334,8 +1336,24 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
         return mvm_check_launch("triplet_small_kernel");
     }
     if (kernel == MVM_CUBE_DEFAULT || kernel == MVM_CUBE_SMALL || kernel == MVM_CUBE_FUSED) {
+        // tiles of 16 i x 32 j; views of <= 64 / <= 128 put four / two (i, j)
+        // rows in every wave instruction; 3 k per lane where the view fits
+        // them (<= 48 / 96 / 192 at four / two / one rows per instruction)
+        const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
+        const int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
+        const int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane
+                                             : (max_n <= 3 * (kWave / split) ? 3 : 4);
+        if (max_n <= kChunk && kpl == 3 && max_n > 3 * (kWave / split))
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
+                            "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
+                            (int)max_n, 3 * (kWave / split));
+        // views of 33-48 at four rows per instruction and 3 k per lane: tiles
+        // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
+        // leaving half of a second 32-wide tile empty
+        const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8;
         const CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
-                                           cube_dev, argmin_dev, minval_dev, max_n, 16);
+                                           cube_dev, argmin_dev, minval_dev, max_n, 16,
+                                           j48 ? 12 : 8);
         const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
         if ((st = grid_check(blocks))) return st;
         const dim3 grid((unsigned)blocks), block(kThreads);
@@ -1344,19 +1362,9 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
             triplet_fused_chunked_kernel<16, 8><<<grid, block, 0, s>>>(c);
             return mvm_check_launch("triplet_fused_chunked_kernel");
         }
-        // tiles of 16 i x 32 j; views of <= 64 / <= 128 put four / two (i, j)
-        // rows in every wave instruction; 3 k per lane where the view fits
-        // them (<= 48 / 96 / 192 at four / two / one rows per instruction)
-        const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
-        const int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
-        const int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane
-                                             : (max_n <= 3 * (kWave / split) ? 3 : 4);
-        if (kpl == 3 && max_n > 3 * (kWave / split))
-            return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
-                            "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
-                            (int)max_n, 3 * (kWave / split));
         if (split == 4) {
-            if (kpl == 3) triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c);
+            if (j48) triplet_fused_kernel<16, 12, 4, 3><<<grid, block, 0, s>>>(c);
+            else if (kpl == 3) triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
         } else if (split == 2) {
             if (kpl == 3) triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c);
