@@ -417,7 +417,8 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // a quarter fewer VALU per row step than 4 k per lane, whose last quarter of
 // lanes would hold no k there; rows are stored with `global_store_dwordx3`.
 template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane>
-__global__ __launch_bounds__(kThreads, kCubeIB <= 16 ? 4 : 2) void triplet_fused_kernel(CubeFusedArgs args) {
+__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2 : kCubeRPW > 8 ? 3 : 4)   // 48-j tiles: 43 KB of LDS, 3 per CU
+void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr bool HALF = SPLIT > 1;   // split mapping
     static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)),
                   "8 or 12 rows in 2 or 4 groups");
