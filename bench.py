@@ -849,13 +849,27 @@ def main():
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for buf in out_slots:
             ops.hbm_write_probe(buf)
+        # per allocation too (an event pair around each probe), so the line
+        # shows whether a slow slot is slow for a plain store stream as well
+        slot_ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                    for _ in out_slots] for _ in range(5)]
         pe0.record(stream)
-        for _ in range(5):
-            for buf in out_slots:
+        for rep in range(5):
+            for i, buf in enumerate(out_slots):
+                slot_ev[rep][i][0].record(stream)
                 ops.hbm_write_probe(buf)
+                slot_ev[rep][i][1].record(stream)
         pe1.record(stream)
         torch.cuda.synchronize(dev)
         probe_gbs = 5 * n_slots * max_units * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
+        if per_slot:
+            for p in per_slot["slots"]:
+                t = float(np.mean([slot_ev[rep][p["slot"]][0].elapsed_time(slot_ev[rep][p["slot"]][1])
+                                   for rep in range(5)])) * 1e-3
+                p["probe_gbs"] = max_units * 4 / t / 1e9
+                p["frac_of_probe"] = p["achieved_gbs"] / p["probe_gbs"]
+            pr = [p["probe_gbs"] for p in per_slot["slots"]]
+            per_slot["probe_fastest_over_slowest"] = max(pr) / min(pr)
 
     units_all = sum_over_ranks(env, units_local)   # ragged shards differ by one scene
     if not env.is_root:
