@@ -473,8 +473,10 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     const int64_t roff = args.row_offs[s];
     // vector rows: every lane's KPL k valid or none (P % KPL == 0); 16-byte
     // aligned for 4 k per lane (dwordx3 stores need 4 bytes)
-    const bool full = (KPL == 4 ? ((P & 3) == 0) && ((coff & 3) == 0) : (P % KPL) == 0) &&
-                      args.cube;
+    // vector rows: 4 k per lane need every lane's 4 k valid or none (P % 4 == 0)
+    // and 16-byte alignment; 3 k per lane need neither (dwordx3 stores are
+    // 4-byte aligned, and the one lane a row ends in stores its 1 or 2 k alone)
+    const bool full = (KPL == 4 ? ((P & 3) == 0) && ((coff & 3) == 0) : true) && args.cube;
     const bool act_k = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
@@ -634,13 +636,21 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
                     for (int q = 0; q < KPL; ++q) v[q] = (float)q0[q];
+                    const bool whole = KPL == 4 || kvalid >= KPL;   // the lane's k all in the row
                     if (act) {
-                        cube_row_store<KPL>(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                            (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
+                        if (whole) {
+                            cube_row_store<KPL>(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
+                                                (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
+                        } else {   // the row's last lane (3 k per lane, P % 3 != 0)
+#pragma unroll
+                            for (int q = 0; q < KPL - 1; ++q)
+                                if (q < kvalid) args.cube[coff + row * P + kb + q] = v[q];
+                        }
                     }
                     Best b{v[0], kb};
 #pragma unroll
-                    for (int q = 1; q < KPL; ++q) best_update_fast(b, v[q], kb + q);
+                    for (int q = 1; q < KPL; ++q)
+                        if (whole || q < kvalid) best_update_fast(b, v[q], kb + q);
                     key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
                     idx[r] = act ? b.j : 0x7FFFFFFF;
                 } else {
