@@ -181,9 +181,9 @@ template <int KPL = kColsPerLane>
 __device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[KPL],
                                                bool lined) {
     static_assert(KPL == 3 || KPL == 4, "3 or 4 k per lane");
-    if constexpr (KPL == 4) {
-        if (lined) store4_nt_row<1>(base, off, v);
-        else store4_nt_row<0>(base, off, v);
+    if constexpr (KPL == 4) {   // rows may be only 4-byte aligned (P % 4 != 0)
+        if (lined) store4_row_a4<1>(base, off, v);
+        else store4_row_a4<0>(base, off, v);
     } else {
         if (lined) store3_row<1>(base, off, v);
         else store3_row<0>(base, off, v);
@@ -473,10 +473,10 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     const int64_t roff = args.row_offs[s];
     // vector rows: every lane's KPL k valid or none (P % KPL == 0); 16-byte
     // aligned for 4 k per lane (dwordx3 stores need 4 bytes)
-    // vector rows: 4 k per lane need every lane's 4 k valid or none (P % 4 == 0)
-    // and 16-byte alignment; 3 k per lane need neither (dwordx3 stores are
-    // 4-byte aligned, and the one lane a row ends in stores its 1 or 2 k alone)
-    const bool full = (KPL == 4 ? ((P & 3) == 0) && ((coff & 3) == 0) : true) && args.cube;
+    // vector rows for any P: a lane stores its KPL k with one dwordx3/x4
+    // (dword-aligned: gfx950 takes it), except the one lane a row ends in
+    // when P % KPL != 0, which stores its 1..KPL-1 k alone
+    const bool full = args.cube != nullptr;
     const bool act_k = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
@@ -636,7 +636,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
                     for (int q = 0; q < KPL; ++q) v[q] = (float)q0[q];
-                    const bool whole = KPL == 4 || kvalid >= KPL;   // the lane's k all in the row
+                    const bool whole = kvalid >= KPL;   // the lane's k all in the row
                     if (act) {
                         if (whole) {
                             cube_row_store<KPL>(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
@@ -947,7 +947,7 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
                 tame_in &= a23[r][q] <= kTameResidual;
             }
         }
-        const bool full = ((P & 3) == 0) && ((coff & 3) == 0) && args.cube;
+        const bool full = args.cube != nullptr;   // any P: see triplet_fused_kernel
         // every sum of this chunk finite: the loop without the per-row vote
         const bool chunk_fast = __syncthreads_and(tame_in) != 0 && full;
         if (nrows <= 0) continue;   // uniform; the barriers above are still reached
@@ -984,13 +984,21 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
                     if (FAST || (full && __all(ok || !act))) {
 #pragma unroll
                         for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)q0[q];
+                        const bool whole = kvalid >= kColsPerLane;
                         if (act) {
-                            cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
-                                          (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
+                            if (whole) {
+                                cube_row_store(reinterpret_cast<uint64_t>(args.cube + coff + row * P + kc),
+                                               (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
+                            } else {   // the row's last lane (P % 4 != 0)
+#pragma unroll
+                                for (int q = 0; q < kColsPerLane - 1; ++q)
+                                    if (q < kvalid) args.cube[coff + row * P + kc + kb + q] = v[q];
+                            }
                         }
                         Best b{v[0], kb};
 #pragma unroll
-                        for (int q = 1; q < kColsPerLane; ++q) best_update_fast(b, v[q], kb + q);
+                        for (int q = 1; q < kColsPerLane; ++q)
+                            if (whole || q < kvalid) best_update_fast(b, v[q], kb + q);
                         key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
                         idx[r] = act ? b.j : 0x7FFFFFFF;
                     } else {

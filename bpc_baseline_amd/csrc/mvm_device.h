@@ -160,6 +160,19 @@ __device__ __forceinline__ void store4_nt_row(uint64_t row_base, uint32_t byte_o
     else
         *reinterpret_cast<g_f32x4 *>(row_base + byte_off) = v;
 }
+// The same 16-byte row store for rows that are only 4-byte aligned (cube rows
+// whose P is not a multiple of 4): gfx950 takes a dword-aligned dwordx4, and
+// the instruction is the same one the aligned form issues.
+typedef f32x4 __attribute__((address_space(1), aligned(4))) g_f32x4a4;
+template <int NT = 1>
+__device__ __forceinline__ void store4_row_a4(uint64_t row_base, uint32_t byte_off, const float v4[4]) {
+    const f32x4 v = {v4[0], v4[1], v4[2], v4[3]};
+    if constexpr (NT == 1)
+        __builtin_nontemporal_store(v, reinterpret_cast<g_f32x4a4 *>(row_base + byte_off));
+    else
+        *reinterpret_cast<g_f32x4a4 *>(row_base + byte_off) = v;
+}
+
 // 3 consecutive outputs of one lane (rows of 3-k lanes): `global_store_dwordx3`,
 // saddr form, 4-byte aligned
 typedef float f32x3 __attribute__((ext_vector_type(3)));
