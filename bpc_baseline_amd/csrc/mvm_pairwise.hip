@@ -168,15 +168,12 @@ __device__ __forceinline__ void pair_bits4(const ColRegs &c, double rl0, double 
 // Lazy argmin: per row a lane keeps only the float32 bits of its minimum over
 // the chunks it has seen -- two v_min3_u32 per 4 pairs; the column is
 // recovered at the end of the row group (lazy_reduce_bits + recovery below)
-// MASKED: the last chunk of a ragged view: a lane stores only the nst columns
-// of its 4 that lie inside the row's pitch (all 4 with one store, 1..3 alone,
-// none past it); the others hold pad-line values (+inf, never a minimum).
-// Rows need only be dword-aligned (unpitched ragged views): gfx950 takes a
-// dword-aligned dwordx4, the same instruction as the aligned form.
+// MASKED: the last chunk of a ragged view, where lanes past the row's pitch
+// (st false) compute pad-line values (+inf, never a minimum) but store nothing.
 template <bool STORE, int NT, bool MASKED = false>
 __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, double rl1, double rl2,
                                               double rx, double ry, float *drow, int jbase,
-                                              uint32_t &bbits, int nst = kColsPerLane) {
+                                              uint32_t &bbits, bool st = true) {
     float v[kColsPerLane];
 #ifdef MVM_DIAG_NO_ARITH   // diagnostic build only (phase timing): the stores without the pair arithmetic
 #pragma unroll
@@ -184,15 +181,7 @@ __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, doub
 #else
     pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
 #endif
-    if (STORE) {
-        if (!MASKED || nst >= kColsPerLane) {
-            store4_row_a4<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
-        } else {
-#pragma unroll
-            for (int q = 0; q < kColsPerLane - 1; ++q)
-                if (q < nst) drow[jbase + q] = v[q];
-        }
-    }
+    if (STORE && (!MASKED || st)) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
     bbits = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2])),
                      __float_as_uint(v[3]), bbits);
 }
@@ -465,7 +454,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
         const bool rows_fast =
             (nrows == RPW) && __all(lane >= RPW || rowp[lane % RPW][5] == 0.0);
         // uniform: the whole group takes the lazy argmin (clean rows and tile)
-        if (tile_clean && rows_fast) {   // any row alignment (row_fast_lazy)
+        if (tile_clean && rows_fast && (vec_ok || !dbase)) {
             uint32_t bbits[RPW];
 #pragma unroll
             for (int r = 0; r < RPW; ++r) bbits[r] = 0x7F800000u;
@@ -473,7 +462,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             auto sweep_chunk = [&](int c0, auto masked) __attribute__((always_inline)) {
                 constexpr bool M = decltype(masked)::value;
                 const int jbase = c0 + kColsPerLane * lane;
-                const int nst = g.lim - jbase;   // columns of the lane's 4 inside the pitch
+                const bool st = jbase < g.lim;
                 ColRegs c;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
@@ -491,7 +480,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                     for (int r = 0; r < RPW; ++r)
                         row_fast_lazy<true, NT, true>(
                             c, rowp[r][0], rowp[r][1], rowp[r][2], rowp[r][3], rowp[r][4],
-                            dbase + (int64_t)(grow0 + r * RST) * g.ld, jbase, bbits[r], nst);
+                            dbase + (int64_t)(grow0 + r * RST) * g.ld, jbase, bbits[r], st);
                 } else if (dbase) {
                     const uint64_t rstep = (uint64_t)g.ld * RST * sizeof(float);
                     uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * g.ld);
