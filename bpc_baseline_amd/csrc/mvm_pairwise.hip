@@ -466,7 +466,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 ColRegs c;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
+#ifdef MVM_DIAG_OCC3_C3   // diagnostic build only (timing): a 640-column LDS tile reused
+                    const int jj = (jbase + q) % args.col_tile;
+#else
                     const int jj = jbase + q;
+#endif
                     c.l0[q] = s_l0[jj];
                     c.l1[q] = s_l1[jj];
                     c.l2[q] = s_l2[jj];
@@ -559,7 +563,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 const int c = idx / kColsPerLane, q = idx % kColsPerLane;
                 if (c < n_ch) {
                     const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
+#ifdef MVM_DIAG_OCC3_C3
+                                                  (c * kChunk + kColsPerLane * w + q) % args.col_tile, rl);
+#else
                                                   c * kChunk + kColsPerLane * w + q, rl);
+#endif
                     first = (b == k) ? (uint32_t)idx : first;
                 }
             }
@@ -573,7 +581,11 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 if (tie) {
                     uint32_t jt = 0xFFFFFFFFu;
                     for (int jj = nb - LPR + seg; jj >= 0; jj -= LPR)
+#ifdef MVM_DIAG_OCC3_C3
+                        jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj % args.col_tile, rl) == k)
+#else
                         jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj, rl) == k)
+#endif
                                  ? (uint32_t)jj : jt;
                     jwin = (int)group_min_u32<RPW>(jt);
                 }
@@ -850,6 +862,9 @@ template <int RPW>
 int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_cols,
                         int row_groups, bool argmin, bool f64, hipStream_t stream) {
     a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
+#ifdef MVM_DIAG_OCC3_C3   // diagnostic build only: LDS small enough for three workgroups per CU
+    if (max_cols > 2 * kChunk && row_groups <= 2) a.col_tile = 640;
+#endif
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);
