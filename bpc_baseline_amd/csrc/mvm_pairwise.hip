@@ -933,20 +933,23 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
     if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
                         (int)o.pairwise_row_groups);
-    // default: ~128 rows per workgroup (never more than the rows a view has),
-    // halved while the grid has fewer than kMinBlocks workgroups for narrow
-    // views: the last round of long-lived workgroups is a tail with idle CUs
-    // (C2, 3,000 matrices of 256 rows: 0.156 -> 0.143 ms per launch; 2,000
-    // scenes x 3 cams: 0.298 vs 0.267 ms, profiles/r03/ab/c2_2000_rowgroups.log).
-    // Wide views (C3) took 256 until round 4: over eleven 25 GB output
-    // allocations on four boxes, 128-row blocks cut the slowest-to-fastest
-    // allocation ratio from 1.12-1.16 to 1.05-1.09 (the concurrent write front
-    // per XCD halves) for +0.5% on the mean launch (profiles/r04/slots/).
+    // default: enough row groups to amortise the column lines over ~256 rows
+    // for views of more than 512 columns, ~128 rows for narrower views, never
+    // more than the rows a view has -- halved to ~128 rows while the grid has
+    // fewer than kMinBlocks workgroups: the last round of long-lived
+    // workgroups is a tail with idle CUs (C2, 3,000 matrices of 256 rows:
+    // 0.156 -> 0.143 ms per launch).  C3 keeps 256: 128-row blocks make the
+    // launch far less sensitive to where its output lies (slowest/fastest
+    // allocation 1.12-1.16 -> 1.05-1.09 over four boxes), but the bench line
+    // itself, on one box, alternating, ran 3.5% slower with them (1.547e12 vs
+    // 1.599-1.605e12, profiles/r04/slots/bench_rowblocks/).  256-column views
+    // take 128 at any grid size (2,000 scenes x 3 cams: 0.298 vs 0.267 ms,
+    // profiles/r03/ab/c2_2000_rowgroups.log).
     const int groups_needed = (max_rows + kWaves * rpw - 1) / (kWaves * rpw);
     const int64_t sp_count = (int64_t)n_scenes * a.n_pairs;
     int rg = o.pairwise_row_groups;
     if (!rg) {
-        const int rows_cap = 128;
+        const int rows_cap = max_cols > 2 * kChunk ? 256 : 128;
         rg = max(1, min(groups_needed, rows_cap / (kWaves * rpw)));
         const int rg_floor = min(rg, max(1, 128 / (kWaves * rpw)));
         while (rg > rg_floor &&
