@@ -434,6 +434,10 @@ def main():
                          "(all ranks' rows, as gathered to rank 0) against the oracle, which each "
                          "rank computes for its own scenes and sends to rank 0 over a gloo group; "
                          "scene: only the last launch's first scene")
+    ap.add_argument("--options", default=None, metavar="FIELD=VALUE,...",
+                    help="mvm_options fields for the launches (include/mvmatch.h; e.g. "
+                         "pairwise_row_groups=2): kernel-path choices that never change results, "
+                         "for A/B runs of the line itself; recorded in config.kernel_options")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group (gloo, host only) and print the "
                          "world each rank joined; no GPU work (tests the launcher on a CPU host)")
@@ -461,6 +465,13 @@ def main():
     global ops
     from bpc_baseline_amd import ops as _ops
     ops = _ops
+    kernel_options = None
+    if args.options:
+        kernel_options = {}
+        for kv in args.options.split(","):
+            k, _, v = kv.partition("=")
+            kernel_options[k.strip()] = v.strip() if k.strip() in ("pairwise_argmin", "cube_kernel") \
+                else int(v)
 
     wl = dict(WORKLOADS[args.workload])
     if args.scenes:
@@ -547,9 +558,11 @@ def main():
             dispatched[0] += 1
         out = out_slots[last_slot[id(c)]][:c.size]
         if wl["mode"] == "pairwise":
-            ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
+            ops.pairwise_residual_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv),
+                                         options=kernel_options)
         else:
-            ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv))
+            ops.triplet_cost_argmin(c.pts, c.cam_offs, c.F, c.plan, out=(out, am, mv),
+                                    options=kernel_options)
 
     # the single association gather (N > 1), in per-launch pieces that overlap
     # the next launch's compute; ragged shards fall back to one gather at the end
@@ -918,6 +931,7 @@ def main():
             "output_gb": n_slots * max_units * 4 / 1e9,
             "units_per_gpu_step": units_local,
             "launch_mode": args.graph,
+            "kernel_options": kernel_options,
             "launch": launch_desc,
             "parallelism": (f"scene-sharded x{world}, association gathered to rank 0 per step "
                             f"({env.backend}{', overlapped per launch' if overlap else ''})")
