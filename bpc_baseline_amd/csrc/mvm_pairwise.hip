@@ -524,42 +524,6 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             // (their columns hold pad lines: +inf, never a minimum)
             const int n_full = g.lim / kChunk;
             int c0 = 0;
-#ifdef MVM_EXP_PAIRED_CHUNKS   // experiment: two full chunks per row (2 KiB per wave per row)
-            if constexpr (OCC <= 2) {   // only where the registers allow (LDS caps it at 2)
-                for (; dbase && c0 + kChunk < nb && c0 + kChunk < n_full * kChunk; c0 += 2 * kChunk) {
-                    const int ja = c0 + kColsPerLane * lane, jb = ja + kChunk;
-                    ColRegs ca, cb;
-#pragma unroll
-                    for (int q = 0; q < kColsPerLane; ++q) {
-                        ca.l0[q] = s_l0[ja + q]; ca.l1[q] = s_l1[ja + q]; ca.l2[q] = s_l2[ja + q];
-                        ca.x[q] = s_x[ja + q]; ca.y[q] = s_y[ja + q];
-                        cb.l0[q] = s_l0[jb + q]; cb.l1[q] = s_l1[jb + q]; cb.l2[q] = s_l2[jb + q];
-                        cb.x[q] = s_x[jb + q]; cb.y[q] = s_y[jb + q];
-                    }
-                    const uint64_t rstep = (uint64_t)g.ld * RST * sizeof(float);
-                    uint64_t rp = reinterpret_cast<uint64_t>(dbase + (int64_t)grow0 * g.ld);
-                    double cur[5], nxt[5];
-#pragma unroll
-                    for (int e = 0; e < 5; ++e) cur[e] = rowp[0][e];
-#pragma unroll
-                    for (int r = 0; r < RPW; ++r) {
-                        if (r + 1 < RPW) {
-#pragma unroll
-                            for (int e = 0; e < 5; ++e) nxt[e] = rowp[r + 1][e];
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-                        row_fast_lazy<true, NT>(ca, cur[0], cur[1], cur[2], cur[3], cur[4],
-                                                reinterpret_cast<float *>(rp), ja, bbits[r]);
-                        row_fast_lazy<true, NT>(cb, cur[0], cur[1], cur[2], cur[3], cur[4],
-                                                reinterpret_cast<float *>(rp), jb, bbits[r]);
-                        rp += rstep;
-                        __asm__ volatile("" : "+s"(rp));
-#pragma unroll
-                        for (int e = 0; e < 5; ++e) cur[e] = nxt[e];
-                    }
-                }
-            }
-#endif
             for (; c0 < nb && c0 < n_full * kChunk; c0 += kChunk) sweep_chunk(c0, std::false_type{});
             if (c0 < nb) sweep_chunk(c0, std::true_type{});
             constexpr int LPR = kWave / RPW;
