@@ -14,6 +14,8 @@ are stored, as arrays.
 Fixtures (all .npz, loaded with allow_pickle=False):
   a1_epipolar_error.npz  scalar epipolar_error / epipolar_error_full KATs (fp64 outputs)
   a3_cost_cubes.npz      compute_cost_matrix cubes + match_objects + argmin rows
+  a3b_cost_cubes_mid.npz compute_cost_matrix cubes at the fused kernel's lane/tile
+                         boundaries (views of 47/48, 97, 150, 250) + argmin rows
   a5_pairwise.npz        4-camera pairwise residual matrices (f32 of epipolar_error)
   a6_fundamental.npz     compute_fundamental_matrix on IPD-like rigs
   a7_match.npz           PoseEstimator._match on synthetic captures (matches, t)
@@ -174,6 +176,40 @@ def gen_a3(em, rng):
         print(f"a3: {name} {cube.shape} matches@30={len(m30)}")
     arrays["names"] = np.asarray([c[0] for c in CUBE_CASES])
     np.savez_compressed(os.path.join(OUT, "a3_cost_cubes.npz"), **arrays)
+
+
+# round 4: views on the fused cube kernel's lane / tile boundaries (3 k per
+# lane with a partial last lane and 48-wide j tiles; P not a multiple of 4 at
+# two and one rows per instruction), from a stream of their own so that the
+# fixtures above regenerate byte-identically
+CUBE_CASES_MID = [
+    ("m48", (20, 48, 47), "rig", 0),
+    ("m97", (10, 30, 97), "rig", 0),
+    ("m150", (4, 20, 150), "rig", 0),
+    ("m250", (3, 10, 250), "rig", 0),
+]
+
+
+def gen_a3b(em, rng):
+    """compute_cost_matrix (:83-98) + the per-row argmin at the boundary sizes above."""
+    from bpc_baseline_amd.inference.utils.camera_utils import fundamental_matrices, camera_pairs
+    arrays = {}
+    for name, counts, _, dup in CUBE_CASES_MID:
+        Ks, RTs, dets = make_capture(rng, 3, list(counts), duplicates=dup)
+        F = fundamental_matrices(Ks, RTs, camera_pairs(3))
+        F12, F13, F23 = (F[p].reshape(3, 3) for p in range(3))
+        cube = em.compute_cost_matrix(dets[0], dets[1], dets[2], F12, F13, F23)
+        assert cube.dtype == np.float32
+        N, M, P = cube.shape
+        arrays[f"{name}_p1"] = _dets_array(dets[0])
+        arrays[f"{name}_p2"] = _dets_array(dets[1])
+        arrays[f"{name}_p3"] = _dets_array(dets[2])
+        arrays[f"{name}_F"] = F
+        arrays[f"{name}_cube"] = cube
+        arrays[f"{name}_argmin"] = np.argmin(cube.reshape(N * M, P), axis=1).astype(np.int32)
+        print(f"a3b: {name} {cube.shape}")
+    arrays["names"] = np.asarray([c[0] for c in CUBE_CASES_MID])
+    np.savez_compressed(os.path.join(OUT, "a3b_cost_cubes_mid.npz"), **arrays)
 
 
 def gen_a5(em, rng):
@@ -369,6 +405,8 @@ def main():
         gen_a8(pp, rng2)
     if want("a9"):
         gen_a9(em, rng2)
+    if want("a3b"):
+        gen_a3b(em, np.random.default_rng(20250511))
 
 
 if __name__ == "__main__":

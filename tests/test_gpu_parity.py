@@ -328,6 +328,22 @@ def test_cube_golden_batched(cuda, golden, cube_path):
         ro += N * M
 
 
+def test_cube_golden_mid_sizes(cuda, golden, cube_path):
+    """The reference's own cubes at the fused kernel's lane / tile boundaries
+    (views of 47/48: 3 k per lane with a partial last lane, 48-wide j tiles;
+    97: 4 k per lane, rows off 16 bytes; 150: 3 k per lane at one row per
+    instruction; 250: rows off 16 bytes at one row per instruction), each in
+    its own launch so each takes its size's kernel, on every cube path."""
+    g = golden("a3b_cost_cubes_mid.npz")
+    _, opts = cube_path
+    for n in g["names"]:
+        p = [g[f"{n}_p{k}"] for k in (1, 2, 3)]
+        cam_offs = np.array([0, len(p[0]), len(p[0]) + len(p[1]), sum(len(x) for x in p)], np.int64)
+        c, a, _ = run_cube(cuda, np.concatenate(p), cam_offs, g[f"{n}_F"], 1, options=opts)
+        assert np.array_equal(_bits(c), _bits(g[f"{n}_cube"].reshape(-1))), f"cube {n}"
+        assert np.array_equal(a, g[f"{n}_argmin"]), f"argmin {n}"
+
+
 @pytest.mark.parametrize("S,n,ragged", [(3, 64, False), (1, 300, False), (4, 45, True), (2, 256, False),
                                         (300, 24, False), (40, 64, True), (7, 1, False),
                                         (2, 512, False), (3, 333, True), (1, 770, False), (2, 200, False),
