@@ -281,10 +281,24 @@ struct BlockGeom {
 // block lies past its matrix's rows (uniform over the workgroup).
 __device__ __forceinline__ bool block_geometry(const PairArgs &args, double (&f)[9], BlockGeom &g) {
     uint32_t blk = blockIdx.x;
+#ifdef MVM_EXP_XCD_BANDS   // experiment: the XCDs walk the grid together, band by band
+    {
+        constexpr uint32_t B = MVM_EXP_XCD_BANDS, SB = 8u * B;
+        const uint32_t nb = gridDim.x, full = nb / SB * SB;
+        if (blk < full) {
+            const uint32_t i = blk / 8, x = blk % 8;
+            blk = i / B * SB + x * B + i % B;
+        } else {
+            const uint32_t rem = nb - full, loc = blk - full, q = rem / 8, r = rem % 8, x = loc % 8;
+            blk = full + x * q + min(x, r) + loc / 8;
+        }
+    }
+#else
     {
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
         blk = x * q + min(x, r) + blk / 8;
     }
+#endif
     const int rb = (int)(blk % (uint32_t)args.row_blocks);
     g.sp = (int)(blk / (uint32_t)args.row_blocks);
     const int s = g.sp / args.n_pairs;
@@ -871,7 +885,11 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     // nontemporal stores for whole-line rows (views of a multiple of 32, or
     // rows pitched to 128-byte lines); rows that end mid-line share that line
     // with the next row, and L2 must merge it (default policy)
+#ifdef MVM_EXP_NO_NT   // experiment: default-policy stores everywhere
+    const bool nt = false;
+#else
     const bool nt = max_cols % 32 == 0 || a.row_align % 32 == 0;
+#endif
     // The default association path: the lazy kernel, for views of one column
     // tile.  Row slots: all of a wave's row groups when they fit in 64 (one
     // up-front row-line pass), else one group's.
