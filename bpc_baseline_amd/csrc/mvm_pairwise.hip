@@ -293,6 +293,14 @@ __device__ __forceinline__ bool block_geometry(const PairArgs &args, double (&f)
             blk = full + x * q + min(x, r) + loc / 8;
         }
     }
+#elif defined(MVM_EXP_XCD_FRONTS)   // experiment: each XCD writes F fronts of its range at once
+    {
+        constexpr uint32_t F = MVM_EXP_XCD_FRONTS;
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8, i = blk / 8;
+        const uint32_t cnt = q + (x < r ? 1u : 0u);
+        const uint32_t loc = cnt % F == 0 ? i % F * (cnt / F) + i / F : i;
+        blk = x * q + min(x, r) + loc;
+    }
 #else
     {
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
