@@ -36,7 +36,7 @@ class MvmOptions(ctypes.Structure):
         "cube_kernel", "cube_rows_per_instr", "lsap_wave_max_cols", "lsap_multi_g",
         "lsap_lds_max_cols", "lsap_lds_small_cols", "lsap_mid_max_cols", "lsap_reg_max_cols",
         "lsap_reg_threads", "lsap_mreg_max_cols", "pairwise_row_interleave",
-        "cube_cols_per_lane")]
+        "cube_cols_per_lane", "pairwise_xcd_fronts")]
 
 
 OPTION_FIELDS = [n for n, _ in MvmOptions._fields_[1:]]

@@ -54,6 +54,7 @@ struct PairArgs {
     int32_t row_stride;         // lazy kernel: row stride within a wave's row group
                                 // (1 contiguous, kWaves interleaved over the waves)
     int32_t row_interleave;     // mvm_options.pairwise_row_interleave (host side)
+    int32_t xcd_fronts;         // contiguous ranges each XCD writes at once (>= 1)
     int32_t pair_a[MVM_MAX_PAIRS];
     int32_t pair_b[MVM_MAX_PAIRS];
 };
@@ -273,40 +274,25 @@ struct BlockGeom {
     int lim;            // columns a row stores: its padding too when pitched
 };
 
-// Dispatch places workgroup b on XCD b % 8; the remap lets each XCD walk a
-// contiguous range of (scene, pair, row block)s, so a (scene, pair)'s row
+// Dispatch places workgroup b on XCD b % 8; the remap gives each XCD a
+// contiguous eighth of the (scene, pair, row block)s, so a (scene, pair)'s row
 // blocks share one L2 for the column points and its output region stays
-// contiguous per XCD.  Every global load here comes before the first store
-// (on CDNA vmcnt orders loads behind earlier stores).  Returns false when the
-// block lies past its matrix's rows (uniform over the workgroup).
+// contiguous per XCD.  With xcd_fronts F > 1 the XCD's eighth is cut into F
+// contiguous ranges walked side by side (its i-th workgroup takes range i % F),
+// so the chip writes 8F fronts at once: the 25 GB C3 launch runs 1-2% faster
+// with F = 4 on the bench line; the XCDs walking the grid together instead
+// (one front) is 7-10% slower.  Every global load here comes
+// before the first store (on CDNA vmcnt orders loads behind earlier stores).
+// Returns false when the block lies past its matrix's rows (uniform over the
+// workgroup).
 __device__ __forceinline__ bool block_geometry(const PairArgs &args, double (&f)[9], BlockGeom &g) {
     uint32_t blk = blockIdx.x;
-#ifdef MVM_EXP_XCD_BANDS   // experiment: the XCDs walk the grid together, band by band
     {
-        constexpr uint32_t B = MVM_EXP_XCD_BANDS, SB = 8u * B;
-        const uint32_t nb = gridDim.x, full = nb / SB * SB;
-        if (blk < full) {
-            const uint32_t i = blk / 8, x = blk % 8;
-            blk = i / B * SB + x * B + i % B;
-        } else {
-            const uint32_t rem = nb - full, loc = blk - full, q = rem / 8, r = rem % 8, x = loc % 8;
-            blk = full + x * q + min(x, r) + loc / 8;
-        }
-    }
-#elif defined(MVM_EXP_XCD_FRONTS)   // experiment: each XCD writes F fronts of its range at once
-    {
-        constexpr uint32_t F = MVM_EXP_XCD_FRONTS;
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8, i = blk / 8;
-        const uint32_t cnt = q + (x < r ? 1u : 0u);
-        const uint32_t loc = cnt % F == 0 ? i % F * (cnt / F) + i / F : i;
-        blk = x * q + min(x, r) + loc;
+        const uint32_t F = (uint32_t)args.xcd_fronts, cnt = q + (x < r ? 1u : 0u);
+        const uint32_t s = cnt / F, fr = i % F;
+        blk = x * q + min(x, r) + fr * s + min(fr, cnt % F) + i / F;
     }
-#else
-    {
-        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
-        blk = x * q + min(x, r) + blk / 8;
-    }
-#endif
     const int rb = (int)(blk % (uint32_t)args.row_blocks);
     g.sp = (int)(blk / (uint32_t)args.row_blocks);
     const int s = g.sp / args.n_pairs;
@@ -956,6 +942,9 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_interleave %d not -1, 0 or 1",
                         (int)o.pairwise_row_interleave);
     a.row_interleave = o.pairwise_row_interleave;
+    if (o.pairwise_xcd_fronts < 0 || o.pairwise_xcd_fronts > 16)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_xcd_fronts %d outside [0, 16]",
+                        (int)o.pairwise_xcd_fronts);
     if (o.pairwise_row_groups < 0 || o.pairwise_row_groups > 16)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "pairwise_row_groups %d outside [0, 16]",
                         (int)o.pairwise_row_groups);
@@ -982,6 +971,12 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
                sp_count * ((max_rows + kWaves * rpw * rg - 1) / (kWaves * rpw * rg)) < kMinBlocks)
             rg /= 2;
     }
+    // 4 write fronts per XCD for launches of >= 8 GB of matrices (C3, 25 GB:
+    // 1.542-1.581e12 -> 1.570-1.600e12 pairs/s on two boxes); the 0.8 GB C2
+    // launch gains nothing (profiles/r04/bench_ab/xcd/)
+    a.xcd_fronts = o.pairwise_xcd_fronts
+                       ? o.pairwise_xcd_fronts
+                       : (double)sp_count * max_rows * max_cols * sizeof(float) >= 8e9 ? 4 : 1;
     const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
     const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
     if (blocks > 0x7FFFFFFFLL)

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 4
+#define MVM_ABI_VERSION 5
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -127,6 +127,10 @@ typedef struct mvm_options {
                                        fits 3 k per lane: <= 48 / 96 / 192 at four / two /
                                        one rows per instruction, else 4); 3 or 4 (ABI 4;
                                        3 on a view that does not fit is an error) */
+    int32_t pairwise_xcd_fronts;    /* 0 default (4 when the launch writes >= 8 GB of
+                                       matrices, else 1); 1..16: each XCD writes its
+                                       eighth of the grid as this many concurrent
+                                       contiguous ranges (ABI 5) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

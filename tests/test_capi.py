@@ -135,6 +135,10 @@ def test_options_init_and_validation(lib):
     st = lib.mvm_pairwise_residual_argmin_ex(FAKE, FAKE, FAKE, pa, pb, 1, 2, 1, 4, FAKE, FAKE,
                                              FAKE, FAKE, FAKE, ctypes.byref(bad), None)
     assert st == 1 and b"rows_per_wave" in lib.mvm_last_error_string()
+    bad = _native.make_options(pairwise_xcd_fronts=17)
+    st = lib.mvm_pairwise_residual_argmin_ex(FAKE, FAKE, FAKE, pa, pb, 1, 2, 1, 4, FAKE, FAKE,
+                                             FAKE, FAKE, FAKE, ctypes.byref(bad), None)
+    assert st == 1 and b"pairwise_xcd_fronts" in lib.mvm_last_error_string()
     bad = _native.make_options(cube_kernel=9)
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(bad), None)

@@ -69,7 +69,8 @@ def assert_pairwise_equal(dev, pts, cam_offs, F, pairs, S, C, options=None):
 
 # ----------------------------------------------------------- pairwise ----
 @pytest.fixture(params=["default", "unpitched", "eager", "eager_unpitched", "rpw8_rg2", "rpw4",
-                        "interleaved", "contiguous", "interleaved_unpitched_rpw8"])
+                        "interleaved", "contiguous", "interleaved_unpitched_rpw8", "fronts3",
+                        "fronts16_unpitched"])
 def argmin_path(request):
     """mvm_options of a pairwise kernel path: the lazy argmin (clean row
     groups: per-chunk minimum bits, column recovered per group through one
@@ -78,7 +79,8 @@ def argmin_path(request):
     over the waves or contiguous per wave (forced either way; the default
     picks by view size) -- each with the plan's default row pitch (128-byte
     lines for ragged views) and some also unpitched (rows of n_b, the
-    unaligned-row paths)."""
+    unaligned-row paths), and the XCD write-front counts forced (3, 16: ranges
+    of unequal length per XCD)."""
     return {"default": {}, "unpitched": {"_row_align": 1},
             "interleaved": {"pairwise_row_interleave": 1},
             "contiguous": {"pairwise_row_interleave": -1},
@@ -87,7 +89,9 @@ def argmin_path(request):
             "eager": {"pairwise_argmin": "eager"},
             "eager_unpitched": {"pairwise_argmin": "eager", "_row_align": 1},
             "rpw8_rg2": {"pairwise_rows_per_wave": 8, "pairwise_row_groups": 2},
-            "rpw4": {"pairwise_rows_per_wave": 4}}[request.param]
+            "rpw4": {"pairwise_rows_per_wave": 4},
+            "fronts3": {"pairwise_xcd_fronts": 3},
+            "fronts16_unpitched": {"pairwise_xcd_fronts": 16, "_row_align": 1}}[request.param]
 
 
 @pytest.mark.parametrize("S,C,n,ragged", [(3, 4, 256, False), (5, 4, 300, True), (2, 4, 1024, False),

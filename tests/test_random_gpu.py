@@ -96,6 +96,8 @@ def test_pairwise_random_vs_oracle(cuda, seed):
     options = [{}, {}, {"pairwise_argmin": "eager"}, {"pairwise_row_interleave": 1},
                {"pairwise_row_interleave": -1}, {"pairwise_rows_per_wave": 8, "pairwise_row_groups": 2},
                {"pairwise_rows_per_wave": 4}][int(rng.integers(0, 7))]
+    if seed % 3 == 0:   # XCD write fronts forced (no rng draw: the sampled cases stay put)
+        options = dict(options, pairwise_xcd_fronts=1 + seed % 7)
     want_dist = rng.random() < 0.85   # else the association alone (no matrices written)
     plan = ops.PairwisePlan(cam_offs, S, C, pairs, device=cuda,
                             row_align=row_align if row_align == "auto" else int(row_align))
