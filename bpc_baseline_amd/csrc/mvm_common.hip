@@ -25,13 +25,7 @@ __global__ __launch_bounds__(kThreads) void write_probe_kernel(f32x4 *dst, size_
     constexpr int kPerLane = 2;
     const f32x4 v = {val, val, val, val};
     const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blockIdx.x % 8;
-#ifdef MVM_EXP_PROBE_FRONTS   // experiment: F write fronts per XCD
-    constexpr uint32_t F = MVM_EXP_PROBE_FRONTS;
-    const uint32_t i = blockIdx.x / 8, cnt = q + (x < r ? 1u : 0u), s = cnt / F, f = i % F;
-    const uint32_t blk = x * q + min(x, r) + f * s + min(f, cnt % F) + i / F;
-#else
     const uint32_t blk = x * q + min(x, r) + blockIdx.x / 8;   // dispatch puts block b on XCD b % 8
-#endif
     const size_t base = (size_t)blk * (kPerLane * kThreads) + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < kPerLane; ++k) {

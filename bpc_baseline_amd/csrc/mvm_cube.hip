@@ -445,13 +445,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     uint32_t blk = blockIdx.x;
     {
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
-#ifdef MVM_EXP_CUBE_FRONTS   // experiment: F write fronts per XCD
-        constexpr uint32_t F = MVM_EXP_CUBE_FRONTS;
-        const uint32_t i = blk / 8, cnt = q + (x < r ? 1u : 0u), s = cnt / F, f = i % F;
-        blk = x * q + min(x, r) + f * s + min(f, cnt % F) + i / F;
-#else
         blk = x * q + min(x, r) + blk / 8;
-#endif
     }
     const uint32_t per_scene = (uint32_t)(args.j_blocks * args.i_blocks);
     const int s = (int)(blk / per_scene);

@@ -879,11 +879,7 @@ int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_col
     // nontemporal stores for whole-line rows (views of a multiple of 32, or
     // rows pitched to 128-byte lines); rows that end mid-line share that line
     // with the next row, and L2 must merge it (default policy)
-#ifdef MVM_EXP_NO_NT   // experiment: default-policy stores everywhere
-    const bool nt = false;
-#else
     const bool nt = max_cols % 32 == 0 || a.row_align % 32 == 0;
-#endif
     // The default association path: the lazy kernel, for views of one column
     // tile.  Row slots: all of a wave's row groups when they fit in 64 (one
     // up-front row-line pass), else one group's.
