@@ -65,13 +65,18 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 METRIC = "detection-pairs matched/sec"
 
 WORKLOADS = {
-    "c3": dict(n_cams=4, n_dets=1024, n_scenes=10000, chunk=1000, mode="pairwise",
+    # C3 launches of 2,000 scenes (50.6 GB of matrices): 1.66e12 pairs/s on
+    # two boxes against 1.57-1.62e12 with 1,000 (fewer launch tails, five
+    # output allocations instead of eleven; profiles/r04/bench_ab/chunk/)
+    "c3": dict(n_cams=4, n_dets=1024, n_scenes=10000, chunk=2000, mode="pairwise",
                desc="C3: synthetic IPD-like 4-cam x 1024 dets/view x 10000 scenes per GPU, "
                     "pairwise residual matrices + per-row argmin"),
     "c2": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=1000, mode="pairwise",
                desc="C2: synthetic IPD-like 3-cam x 256 dets/view x 1000 scenes per GPU, "
                     "pairwise residual matrices + per-row argmin"),
-    "c2cube": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=250, mode="cube",
+    # the cube step as one 16.9 GB launch: 1.76-1.77e12 triples/s against
+    # 1.63-1.66e12 as four of 250 scenes (profiles/r04/bench_ab/chunk/)
+    "c2cube": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=1000, mode="cube",
                    desc="C2 cube: 3-cam x 256 dets/view x 1000 scenes per GPU, "
                         "compute_cost_matrix cubes + per-(i,j) argmin (units = triples)"),
 }
