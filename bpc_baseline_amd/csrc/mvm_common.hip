@@ -94,13 +94,16 @@ int mvm_hbm_write_probe(void *dst_dev, size_t bytes, mvm_stream_t stream) {
     mvm_clear_error();
     if (!dst_dev || (((uintptr_t)dst_dev) & 15) || (bytes & 15))
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "write probe needs a 16-byte aligned buffer/size");
-    const size_t n16 = bytes / 16;
-    const size_t blocks = (n16 + 2 * kThreads - 1) / (2 * kThreads);
-    if (blocks == 0) return MVM_OK;
-    if (blocks > 0x7FFFFFFFull) return mvm_fail(MVM_ERR_UNSUPPORTED, "write probe buffer too large");
-    write_probe_kernel<<<(unsigned)blocks, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        reinterpret_cast<f32x4 *>(dst_dev), n16, 1.0f);
-    return mvm_check_launch("write_probe_kernel");
+    // one launch per piece of at most kMaxGridBlocks workgroups (~137 GB)
+    constexpr size_t kPiece = (size_t)kMaxGridBlocks / 8 * 8 * (2 * kThreads);   // f32x4 per launch
+    for (size_t done = 0, n16 = bytes / 16; done < n16; done += kPiece) {
+        const size_t n = n16 - done < kPiece ? n16 - done : kPiece;
+        const size_t blocks = (n + 2 * kThreads - 1) / (2 * kThreads);
+        write_probe_kernel<<<(unsigned)blocks, kThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+            reinterpret_cast<f32x4 *>(dst_dev) + done, n, 1.0f);
+        if (const int st = mvm_check_launch("write_probe_kernel")) return st;
+    }
+    return MVM_OK;
 }
 
 }  // extern "C"

@@ -1258,7 +1258,7 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
 }
 
 int grid_check(int64_t blocks) {
-    if (blocks > 0x7FFFFFFFLL)
+    if (blocks > kMaxGridBlocks)
         return mvm_fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                         (long long)blocks);
     return MVM_OK;

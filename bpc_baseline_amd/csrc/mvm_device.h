@@ -21,6 +21,9 @@ namespace {
 
 constexpr int kWave = 64;
 constexpr int kThreads = 256;                  // 4 waves per workgroup
+// A dispatch packet counts work-items in 32 bits per dimension: a 1-D grid of
+// 256-thread workgroups holds at most this many (larger launches must split)
+constexpr long long kMaxGridBlocks = 0xFFFFFFFFLL / kThreads;
 constexpr int kWaves = kThreads / kWave;
 constexpr int kColsPerLane = 4;                // one 16-byte store per lane per row
 constexpr int kChunk = kWave * kColsPerLane;   // 256 columns per chunk (== kThreads)

@@ -975,7 +975,7 @@ int launch_pairwise_common(PairArgs &a, int32_t n_scenes, int32_t max_rows, int3
                        : (double)sp_count * max_rows * max_cols * sizeof(float) >= 8e9 ? 4 : 1;
     const int64_t rows_per_wg = (int64_t)kWaves * rpw * rg;
     const int64_t blocks = sp_count * ((max_rows + rows_per_wg - 1) / rows_per_wg);
-    if (blocks > 0x7FFFFFFFLL)
+    if (blocks > kMaxGridBlocks)
         return mvm_fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
                         (long long)blocks);
     int st;

@@ -125,6 +125,16 @@ def test_library_reads_no_environment():
     assert b"getenv\x00" not in blob      # no imported getenv / secure_getenv symbol name
 
 
+def test_grid_beyond_the_dispatch_limit(lib):
+    """A dispatch packet counts work-items in 32 bits: a pairwise batch of
+    more than 2^32 / 256 workgroups is refused, not launched truncated
+    (2,000,000 scenes x 28 pairs x 4 row blocks = 224M workgroups)."""
+    pa, pb = _pairs(*[(a, b) for a in range(8) for b in range(a + 1, 8)])
+    st = lib.mvm_pairwise_residual_argmin_ex(FAKE, FAKE, FAKE, pa, pb, 2_000_000, 8, 28, 1024, FAKE,
+                                             FAKE, FAKE, FAKE, FAKE, None, None)
+    assert st == 2 and b"split the scenes" in lib.mvm_last_error_string()
+
+
 def test_options_init_and_validation(lib):
     o = _native.MvmOptions()
     lib.mvm_options_init(ctypes.byref(o))
