@@ -1969,6 +1969,11 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "lsap_multi_g %d > %d", (int)o.lsap_multi_g, kMultiMaxG);
     if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
     if (n_problems == 0) return MVM_OK;
+    // one workgroup of up to 1024 threads per problem: the dispatch packet's
+    // 32-bit work-item count bounds the batch
+    if ((int64_t)n_problems * kLsapThreads > 0xFFFFFFFFLL)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "%d problems in one batch: split it (at most %lld)",
+                        (int)n_problems, 0xFFFFFFFFLL / kLsapThreads);
     // cost / row_ind / col_ind may be NULL when every problem is empty
     if (!cost_offs_dev || !dims_dev || !ws_offs_dev || !out_offs_dev || !status_dev)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");

@@ -133,6 +133,9 @@ def test_grid_beyond_the_dispatch_limit(lib):
     st = lib.mvm_pairwise_residual_argmin_ex(FAKE, FAKE, FAKE, pa, pb, 2_000_000, 8, 28, 1024, FAKE,
                                              FAKE, FAKE, FAKE, FAKE, None, None)
     assert st == 2 and b"split the scenes" in lib.mvm_last_error_string()
+    st = lib.mvm_lsap_solve_ex(FAKE, 0, FAKE, FAKE, 5_000_000, FAKE, FAKE, FAKE, 1 << 20, FAKE, FAKE,
+                               FAKE, 1, 1, None, None)
+    assert st == 2 and b"split it" in lib.mvm_last_error_string()
 
 
 def test_options_init_and_validation(lib):
