@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X multi-view epipolar matcher (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c2cube]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c2cube|c2match]
 
 A *step* is one pass of the hot path over this rank's whole batch of
 synthetic scenes (resident in HBM): pairwise symmetric epipolar residuals for
@@ -30,11 +30,16 @@ every rank checks that the process group it joined has N ranks.  After the
 timed region every association row of the last step -- all ranks' rows, as
 gathered to rank 0 -- is compared with the CPU oracle (``parity_rows``).
 By default every launch of the timed steps writes its own output allocation
-as far as HBM holds them (C3: ten 25 GB buffers, 252 GB, one per launch of a
-step; C2: one per step), taken round robin, so a step's outputs all stay
-resident and the measurement covers much of the HBM rather than wherever one
-launch-sized buffer happened to land (the same launch runs up to ~20% apart
-on different allocations: DESIGN.md §5); ``--output ring`` reuses one buffer.
+as far as HBM holds them (C3: five launches of 2,000 scenes into five 50 GB
+buffers, 253 GB, one per launch of a step; C2: one per step), taken round
+robin, so a step's outputs all stay resident and the measurement covers much
+of the HBM rather than wherever one launch-sized buffer happened to land (the
+same launch runs up to ~20% apart on different allocations: DESIGN.md §5);
+``--output ring`` reuses one buffer.  The first scene of the launch each
+allocation last held is compared with the oracle bit for bit (``parity``).
+
+``--workload c2match`` times what ``match_objects`` returns at C2 scale (cube +
+scipy-identical assignment + threshold/sort/DLT, units = captures).
 
 Printed by rank 0: ONE JSON line with value = total pairs/s over all ranks,
 the dominant kernel's roofline (achieved algorithmic GB/s from HIP events on
@@ -79,6 +84,11 @@ WORKLOADS = {
     "c2cube": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=1000, mode="cube",
                    desc="C2 cube: 3-cam x 256 dets/view x 1000 scenes per GPU, "
                         "compute_cost_matrix cubes + per-(i,j) argmin (units = triples)"),
+    # what match_objects returns at C2 scale: cube + Hungarian + select/DLT
+    "c2match": dict(n_cams=3, n_dets=256, n_scenes=1000, chunk=1000, mode="match", threshold=30.0,
+                    desc="C2 match: 3-cam x 256 dets/view x 1000 scenes per GPU: "
+                         "compute_cost_matrix cubes, scipy-identical linear_sum_assignment of "
+                         "every (N*M, P) cube, threshold + cost sort + DLT (units = captures)"),
 }
 
 
@@ -130,6 +140,7 @@ def build_chunks(batch, bounds, device, mode):
             nbytes = cube_bytes(counts[s0:s1])
         chunks.append(Chunk(s0, pts, torch.from_numpy(co_rel).to(device), F, plan, row_base, units,
                             size, nbytes))
+        chunks[-1].idx = len(chunks) - 1
         row_base += plan.n_rows
     return chunks, row_base
 
@@ -146,6 +157,8 @@ def cpu_model() -> str:
 
 
 def cpu_threads() -> int:
+    """This rank's threads (affinity, capped by OMP_NUM_THREADS): what the
+    post-timing oracle runs of every rank use side by side."""
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     omp = os.environ.get("OMP_NUM_THREADS")
     if omp and omp.isdigit():
@@ -153,11 +166,40 @@ def cpu_threads() -> int:
     return max(1, int(n))
 
 
+def host_cpu_threads() -> tuple:
+    """Threads of the CPU baseline, the same at every N: the host cores this
+    process may use (affinity, capped by the cgroup's CPU quota) capped by the
+    OMP_NUM_THREADS the *host* sets.  A launcher's per-rank value is ignored:
+    ``launch_ranks`` hands the host's own value down as MVM_HOST_OMP_THREADS,
+    and torchrun's injected OMP_NUM_THREADS=1 at world > 1 is not a host
+    setting.  -> (threads, how they were chosen)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    src = [f"affinity {n}"]
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            quota, period = fh.read().split()[:2]
+        if quota != "max":
+            q = max(1, -(-int(quota) // int(period)))
+            n = min(n, q)
+            src.append(f"cgroup quota {q}")
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("MVM_HOST_OMP_THREADS")
+    if omp is None:
+        omp = os.environ.get("OMP_NUM_THREADS")
+        if omp == "1" and int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            omp = None                       # torchrun's per-rank default, not the host's
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+        src.append(f"host OMP_NUM_THREADS {omp}")
+    return max(1, int(n)), ", ".join(src)
+
+
 def cpu_baseline(batch, mode: str, target_s: float):
     """Time the C/OpenMP restatement (oracle/, test infrastructure) on a bounded
     sample of this workload's scenes -> dict for the JSON line."""
     from oracle import oracle as O
-    threads = cpu_threads()
+    threads, threads_src = host_cpu_threads()
     C = batch.n_cams
 
     def run(n_sc, nthreads=threads):
@@ -214,7 +256,8 @@ def cpu_baseline(batch, mode: str, target_s: float):
     extra["reference_loop_value"] = n_ref / s_ref if s_ref else None
     extra["reference_loop_sample"] = (f"{n_ref} {unit[:-2]} in {s_ref:.1f} s, oracle/reference_loop.py "
                                       "(the reference's per-pair NumPy calls in Python loops, one core)")
-    return {"value": units / secs, "unit": unit, "cores": threads, "kind": "port",
+    return {"value": units / secs, "unit": unit, "cores": threads, "cores_at_n1": threads,
+            "cores_source": threads_src + " (independent of the rank count)", "kind": "port",
             "one_core_value": u1 / s1, "one_core_sample": f"{n1} scenes in {s1:.1f} s", **extra,
             "sample": f"{n_sc} scenes ({units:.3g} {unit[:-2]}) of this workload in {secs:.1f} s, "
                       f"oracle/mvm_oracle.c fp64 restatement (bit-exact to the reference), "
@@ -369,6 +412,54 @@ def launch_bounds(n_local: int, chunk: int, min_launches: int, tail_frac: float 
     return main + ([(n_local - tail, n_local)] if tail else [])
 
 
+def compare_rows_streamed(env, ref_am: np.ndarray, ref_mv: np.ndarray, g_am, g_mv):
+    """Every rank's oracle rows against rank 0's gathered rows, bit for bit.
+
+    Rank r (> 0) sends its oracle rows to rank 0 over the host (gloo) group,
+    one rank at a time, and rank 0 compares them with rank r's slice of what
+    the step's gather delivered: rank 0 holds at most one other rank's rows
+    at once (not the whole job's).  -> (rows, rows equal, first unequal
+    global row or None) on rank 0; (0, 0, None) elsewhere."""
+    if not env.initialised:
+        total = int(ref_am.size)
+        if g_am.size != total:
+            return total, 0, 0
+        eq = (g_am == ref_am) & (g_mv.view(np.int32) == ref_mv.view(np.int32))
+        bad = np.flatnonzero(~eq)
+        return total, int(eq.sum()), (int(bad[0]) if bad.size else None)
+    import torch.distributed as dist
+    grp = env.cpu_group()
+    n = torch.tensor([ref_am.size], dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(env.world)]
+    dist.all_gather(sizes, n, group=grp)
+    sizes = [int(s.item()) for s in sizes]
+    if not env.is_root:
+        dist.send(torch.from_numpy(np.ascontiguousarray(ref_am)), dst=0, group=grp)
+        dist.send(torch.from_numpy(np.ascontiguousarray(ref_mv)), dst=0, group=grp)
+        return 0, 0, None
+    total, ok, first_bad, base = sum(sizes), 0, None, 0
+    for r, nr in enumerate(sizes):
+        if r == 0:
+            am, mv = ref_am, ref_mv
+        else:
+            am_t = torch.empty(nr, dtype=torch.int32)
+            mv_t = torch.empty(nr, dtype=torch.float32)
+            dist.recv(am_t, src=r, group=grp)
+            dist.recv(mv_t, src=r, group=grp)
+            am, mv = am_t.numpy(), mv_t.numpy()
+        if g_am.size == total:
+            ga, gm = g_am[base:base + nr], g_mv[base:base + nr]
+            eq = (ga == am) & (gm.view(np.int32) == mv.view(np.int32))
+            ok += int(eq.sum())
+            bad = np.flatnonzero(~eq)
+            if bad.size and first_bad is None:
+                first_bad = base + int(bad[0])
+        elif first_bad is None:
+            first_bad = 0
+        base += nr
+    return total, ok, first_bad
+
+
 def launch_ranks(n: int) -> int:
     """``--gpus N`` (N > 1) started without a launcher: run this same command
     as N ranks under torchrun in a CHILD process (this parent has made no GPU
@@ -383,6 +474,9 @@ def launch_ranks(n: int) -> int:
     s.close()
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")     # dmabuf IPC (RCCL)
+    # the host's own thread setting, for rank 0's CPU baseline after the timed
+    # region (the same at every N); each rank's OpenMP gets a share of the host
+    env["MVM_HOST_OMP_THREADS"] = str(host_cpu_threads()[0])
     if "OMP_NUM_THREADS" not in env:                     # torchrun would set 1
         env["OMP_NUM_THREADS"] = str(max(1, min(16, cpu_threads() // n)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
@@ -399,6 +493,196 @@ def launch_ranks(n: int) -> int:
     if rc != 0:
         log(f"error: the {n}-rank run exited with status {rc}")
     return rc
+
+
+def match_cpu_chain(batch, proj, s: int, threshold: float, nthreads: int = 1):
+    """Scene s through the CPU restatements, as the reference computes it
+    (epipolar_matching.py:83-116, process_pose.py:182-187): the oracle cube
+    (C), the assignment (scipy, the reference's own call; oracle/lsap.py's
+    restatement of it when scipy is absent), threshold, stable sort by cost,
+    DLT (numpy SVD).  -> (cube, row_ind, col_ind, matches, X)."""
+    from oracle import oracle as O
+    from oracle import pipeline as OP
+    try:
+        from scipy.optimize import linear_sum_assignment as lsa
+    except ImportError:                                     # pragma: no cover
+        from oracle.lsap import linear_sum_assignment as lsa
+    co = batch.cam_offs[3 * s:3 * s + 4]
+    pts = batch.pts[int(co[0]):int(co[3])]
+    n = np.diff(co)
+    cube = O.cube(pts, co - co[0], batch.F[3 * s:3 * s + 3], 1, nthreads=nthreads)[0]
+    flat = cube.reshape(n[0] * n[1], n[2])
+    r, c = lsa(flat)
+    m = [(int(i) // n[1], int(i) % n[1], int(k)) for i, k in zip(r, c) if flat[i, k] < threshold]
+    m = sorted(m, key=lambda t: cube.reshape(n)[t])
+    rel = co[:3] - co[0]
+    X = (OP.triangulate(np.repeat(proj[s][None], len(m), 0),
+                        np.stack([pts[rel + np.array(t)] for t in m]))
+         if m else np.zeros((0, 3)))
+    return cube, np.asarray(r), np.asarray(c), m, X
+
+
+def run_match(args, env, wl, kernel_options):
+    """The ``c2match`` workload: what ``match_objects`` returns, at C2 scale.
+
+    A step is every scene of this rank through the device chain of
+    ``batch_match.match_captures`` with its plans built once (the counts are
+    host knowledge): the compute_cost_matrix cube (mvm_triplet_cost_argmin),
+    scipy's linear_sum_assignment of every flattened (N*M, P) cube
+    (mvm_lsap_solve), then threshold + stable cost sort + DLT
+    (mvm_select_triangulate) -- epipolar_matching.py:83-116 and
+    process_pose.py:182-187.  Units are captures (scenes); HIP events time
+    each stage.  After timing, a few scenes are checked against the CPU chain:
+    the cube bit for bit, the assignment pair for pair, the matches and their
+    order exactly and the triangulated points to 1e-10."""
+    from bpc_baseline_amd.distributed import shard_range
+    from bpc_baseline_amd.inference.utils.camera_utils import projection_matrices
+    dev, world = env.device, env.world
+    if args.scaling == "weak":
+        first, n_local = env.rank * wl["n_scenes"], wl["n_scenes"]
+    else:
+        a, b = shard_range(wl["n_scenes"], env.rank, world)
+        first, n_local = a, b - a
+    t0 = time.perf_counter()
+    batch = make_scenes(n_local, 3, wl["n_dets"], seed=args.seed, first_scene=first)
+    proj = projection_matrices(batch.meta["Ks"], batch.meta["RTs"])
+    log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
+    pts = torch.from_numpy(batch.pts).to(dev)
+    cam_offs = torch.from_numpy(batch.cam_offs).to(dev)
+    F = torch.from_numpy(batch.F).to(dev)
+    proj_d = torch.from_numpy(proj).to(dev)
+    tplan = ops.TripletPlan(batch.cam_offs, n_local, device=dev)
+    c3 = tplan.counts
+    lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+    cube = torch.empty(tplan.n_cube, dtype=torch.float32, device=dev)
+    am = torch.empty(tplan.n_rows, dtype=torch.int32, device=dev)
+    mv = torch.empty(tplan.n_rows, dtype=torch.float32, device=dev)
+    offs = tplan.cube_offs[:-1].contiguous()
+    threshold = float(wl["threshold"])
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record(stream)
+        ops.triplet_cost_argmin(pts, cam_offs, F, tplan, out=(cube, am, mv), options=kernel_options)
+        if ev:
+            ev[1].record(stream)
+        r, c, st = ops.linear_sum_assignment_batched(cube, offs, lplan, options=kernel_options)
+        if ev:
+            ev[2].record(stream)
+        res = ops.select_triangulate(cube, tplan.cube_offs, cam_offs, lplan.out_offs, r, c, pts,
+                                     proj_d, threshold)
+        if ev:
+            ev[3].record(stream)
+        return (r, c, st) + tuple(res)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    env.barrier()
+    torch.cuda.synchronize(dev)
+    with ClockSampler(dev) as clocks:
+        t_start = time.perf_counter()
+        for s in range(args.steps):
+            out = step(evs[s])
+        torch.cuda.synchronize(dev)
+        env.barrier()
+        elapsed = time.perf_counter() - t_start
+    elapsed = max_over_ranks(env, elapsed)
+    stage = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])]
+                      for e in evs])                          # ms per step: cube, lsap, select
+    cube_ms, lsap_ms, sel_ms = (float(x) for x in stage.mean(axis=0))
+    r, c, st, match, cost, X, count = out
+    status = st.cpu().numpy()
+    count_h = count.cpu().numpy()
+    n_matches = sum_over_ranks(env, int(count_h.sum()))
+
+    # ---- parity (untimed): a few scenes against the CPU chain --------------
+    parity_ok, detail = bool((status == 0).all()), []
+    if env.is_root:
+        r_h, c_h = r.cpu().numpy(), c.cpu().numpy()
+        m_h, X_h = match.cpu().numpy(), X.cpu().numpy()
+        picks = sorted({0, n_local // 3, (2 * n_local) // 3, n_local - 1})
+        for s in picks:
+            rc, rr, rcol, rm, rX = match_cpu_chain(batch, proj, s, threshold,
+                                                   nthreads=cpu_threads())
+            o = int(tplan.cube_offs_host[s])
+            cube_ok = np.array_equal(cube[o:o + rc.size].cpu().numpy().view(np.int32), rc.view(np.int32))
+            lo = int(lplan.out_offs_host[s])
+            nn = rr.size
+            lsap_ok = (np.array_equal(r_h[lo:lo + nn], rr) and np.array_equal(c_h[lo:lo + nn], rcol))
+            k = int(count_h[s])
+            got = [tuple(int(v) for v in m_h[lo + w]) for w in range(k)]
+            match_ok = got == rm
+            x_ok = match_ok and (k == 0 or np.allclose(X_h[lo:lo + k], rX, rtol=1e-10, atol=1e-9))
+            parity_ok &= bool(cube_ok and lsap_ok and match_ok and x_ok)
+            detail.append({"scene": first + s, "cube_bit_exact": bool(cube_ok),
+                           "assignment_equal": bool(lsap_ok), "matches": k,
+                           "matches_equal_in_order": bool(match_ok), "X_within_1e-10": bool(x_ok)})
+    if not env.is_root:
+        return
+    total = n_local * world if args.scaling == "weak" else wl["n_scenes"]
+    value = total * args.steps / elapsed
+    counts = batch.counts()
+    cb = cube_bytes(counts)
+    # every cost entry must be read at least once by any exact assignment:
+    # that floor is the assignment stage's algorithmic traffic
+    lsap_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
+    stages = {"cube": (cube_ms, cb, "triplet_fused_kernel"),
+              "lsap": (lsap_ms, lsap_bytes, "mvm_lsap_solve kernels"),
+              "select": (sel_ms, 0.0, "select_triangulate_kernel")}
+    dom = max(stages, key=lambda k: stages[k][0])
+    d_ms, d_bytes, d_kernel = stages[dom]
+    achieved = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else None
+    cpu = None
+    if args.cpu_seconds > 0:
+        threads, threads_src = host_cpu_threads()
+        match_cpu_chain(batch, proj, 0, threshold, nthreads=threads)      # warm
+        n_cpu, t0 = 0, time.perf_counter()
+        while n_cpu < n_local and time.perf_counter() - t0 < args.cpu_seconds:
+            match_cpu_chain(batch, proj, n_cpu, threshold, nthreads=threads)
+            n_cpu += 1
+        secs = time.perf_counter() - t0
+        cpu = {"value": n_cpu / secs, "unit": "captures/s", "cores": threads,
+               "cores_at_n1": threads, "cores_source": threads_src, "kind": "port",
+               "sample": (f"{n_cpu} scenes in {secs:.1f} s: oracle/mvm_oracle.c cube (OpenMP "
+                          f"x{threads}) + scipy.optimize.linear_sum_assignment (the reference's "
+                          "own call, one core) + threshold/sort + numpy SVD per match, on "
+                          f"{cpu_model()}")}
+    line = {
+        "metric": "captures matched/sec (cost cube + scipy-identical assignment + select/DLT)",
+        "value": value, "unit": "captures/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded IPD-like rig, SURVEY §8d generator)",
+        "config": {"workload": wl["desc"], "n_cams": 3, "n_dets": wl["n_dets"],
+                   "n_scenes_per_gpu": n_local, "n_scenes_total": total,
+                   "matching_threshold": threshold, "kernel_options": kernel_options,
+                   "launch": "eager op calls (the assignment's launch is cooperative)",
+                   "parallelism": f"scene-sharded x{world}" if env.initialised else "single GPU"},
+        "stages_ms": {"cube": cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
+                      "note": "rank 0, HIP events on the launch stream, mean over the timed steps"},
+        "lsap": {"problems": n_local, "shape": f"{int(counts[0, 0] * counts[0, 1])} x {int(counts[0, 2])}",
+                 "ms_per_batch": lsap_ms, "ms_per_problem": lsap_ms / max(1, n_local),
+                 "cost_gb_read_floor": lsap_bytes / 1e9},
+        "matches_per_step": n_matches,
+        "sclk": clocks.summary("sclk"),
+        "roofline": {"bound": "hbm", "stage": dom, "kernel": d_kernel, "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                     "bytes_per_launch": d_bytes, "avg_launch_ms": d_ms,
+                     "note": ("the slowest stage; its algorithmic bytes: the cube's writes (4 B "
+                              "per triple + 8 B per row + inputs), or for the assignment the cost "
+                              "cube read once (4 B per entry)")},
+        "cpu_baseline": cpu,
+        "parity": f"{'equal' if parity_ok else 'MISMATCH'} vs the CPU chain on {len(detail)} scenes",
+        "parity_detail": detail,
+    }
+    print(json.dumps(line), flush=True)
+    if not parity_ok:
+        log("error: c2match parity")
+        raise SystemExit(3)
 
 
 def main():
@@ -493,6 +777,8 @@ def main():
     if env.backend == "nccl" and torch.cuda.device_count() < world:
         raise SystemExit(f"error: {world} RCCL ranks but {torch.cuda.device_count()} visible GPU(s)")
     dev = env.device
+    if wl["mode"] == "match":
+        return run_match(args, env, wl, kernel_options)
     if args.graph == "auto":
         # per-launch replays (and the per-launch HIP events around them) cost the
         # host ~15 us per replay; a 0.14 ms C2 launch cannot hide that, C3's
@@ -545,19 +831,16 @@ def main():
     n_slots = len(out_slots)
     seq = [0]             # launches issued (or captured) so far: the next slot
     last_slot = {}        # chunk -> the slot its latest launch wrote
+    slot_owner = {}       # slot -> index of the chunk whose output it holds
     dispatched = [0]      # kernel launches that reached the GPU (rocprof window, below)
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
-
-    def out_of(c: Chunk):
-        """The chunk's residuals in the unpitched layout."""
-        out = out_slots[last_slot[id(c)]][:c.size]
-        return c.plan.compact(out) if wl["mode"] == "pairwise" else out
 
     def launch(c: Chunk):
         am = argmin[c.row_base:c.row_base + c.plan.n_rows]
         mv = minval[c.row_base:c.row_base + c.plan.n_rows]
         last_slot[id(c)] = seq[0] % n_slots
+        slot_owner[last_slot[id(c)]] = c.idx
         seq[0] += 1
         if not torch.cuda.is_current_stream_capturing():
             dispatched[0] += 1
@@ -630,6 +913,7 @@ def main():
         if graphs is not None:
             graphs[s][k].replay()
             dispatched[0] += 1
+            slot_owner[graph_slot[(s, k)]] = k
             return graph_slot[(s, k)]
         launch(chunks[k])
         return last_slot[id(chunks[k])]
@@ -765,24 +1049,19 @@ def main():
             _, ra, rm, _, _ = O.cube(batch.pts, batch.cam_offs, batch.F, batch.n_scenes,
                                      want_cube=False, nthreads=nth)
         t_oracle = max_over_ranks(env, time.perf_counter() - t0)
-        ref = gather_rows(env, torch.from_numpy(ra), torch.from_numpy(rm), group=env.cpu_group())
+        g_am = g_mv = None
         if env.is_root:
             if env.initialised:
                 g_am, g_mv = (g.reshape(-1).cpu().numpy() for g in gathered[:2])
             else:
                 g_am, g_mv = argmin.cpu().numpy(), minval.cpu().numpy()
-            r_am, r_mv = ref[0].numpy(), ref[1].numpy()
-            total = int(r_am.size)
-            if g_am.size != total:
-                ok_rows, first_bad = 0, 0
-            else:
-                eq = (g_am == r_am) & (g_mv.view(np.int32) == r_mv.view(np.int32))
-                ok_rows = int(eq.sum())
-                bad = np.flatnonzero(~eq)
-                first_bad = int(bad[0]) if bad.size else None
+        total, ok_rows, first_bad = compare_rows_streamed(env, ra, rm, g_am, g_mv)
+        if env.is_root:
             parity_rows = f"{ok_rows}/{total} bit-exact vs oracle"
             parity_detail = {
                 "rows_checked": total, "rows_bit_exact": ok_rows, "gathered_rows": int(g_am.size),
+                "transfer": "oracle rows sent to rank 0 one rank at a time (gloo send/recv) and "
+                            "compared with that rank's slice of the gathered rows",
                 "first_mismatch_row": first_bad, "ranks": world, "oracle_threads_per_rank": nth,
                 "oracle_s": t_oracle,
                 "what": ("every (argmin, min) row of the last timed step, in global scene order: "
@@ -801,33 +1080,36 @@ def main():
         np.save(os.path.join(args.dump_association, "argmin.npy"), g_am)
         np.save(os.path.join(args.dump_association, "minval.npy"), g_mv)
 
-    # ---- parity spot-check of the last launch (untimed) --------------------
-    parity = "skipped"
-    if env.is_root and wl["mode"] == "pairwise":
+    # ---- residual matrices vs the oracle (untimed): the first scene of the
+    # launch whose output each allocation still holds, so every allocation the
+    # last step wrote is checked (C3: five scenes, five 50 GB allocations) ----
+    parity, parity_ok = "skipped", True
+    if env.is_root:
         from oracle import oracle as O
-        c = chunks[-1]          # its residuals are still in its output slot
-        s_first = c.s0
-        C = batch.n_cams
-        co = batch.cam_offs[s_first * C:(s_first + 1) * C + 1]
-        co_rel = co - co[0]
-        rd, ra, _, _, _ = O.pairwise(batch.pts[int(co[0]):int(co[-1])], co_rel,
-                                     batch.F[s_first * batch.n_pairs:(s_first + 1) * batch.n_pairs],
-                                     batch.pairs, 1, C)
-        gd = out_of(c)[:rd.size].cpu().numpy()
-        ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
-        ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
-        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {first + s_first} ({rd.size} pairs)"
-    elif env.is_root:
-        from oracle import oracle as O
-        c = chunks[-1]          # its cube is still in its output slot
-        s_first = c.s0
-        co = batch.cam_offs[s_first * 3:(s_first + 1) * 3 + 1]
-        rc, ra, _, _, _ = O.cube(batch.pts[int(co[0]):int(co[-1])], co - co[0],
-                                 batch.F[s_first * 3:(s_first + 1) * 3], 1)
-        gc = out_of(c)[:rc.size].cpu().numpy()
-        ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
-        ok = np.array_equal(gc.view(np.int32), rc.view(np.int32)) and np.array_equal(ga, ra)
-        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on scene {first + s_first} ({rc.size} triples)"
+        C, P = batch.n_cams, batch.n_pairs
+        n_units, checked = 0, []
+        for sl in sorted(slot_owner):
+            c = chunks[slot_owner[sl]]
+            s_first = c.s0
+            co = batch.cam_offs[s_first * C:(s_first + 1) * C + 1]
+            pts1 = batch.pts[int(co[0]):int(co[-1])]
+            out = out_slots[sl]
+            if wl["mode"] == "pairwise":
+                rd, ra, _, _, _ = O.pairwise(pts1, co - co[0], batch.F[s_first * P:(s_first + 1) * P],
+                                             batch.pairs, 1, C)
+                # the scene's matrices, unpitched, read through the plan's offsets
+                gd = torch.cat([c.plan.matrix(out, 0, p).reshape(-1) for p in range(P)]).cpu().numpy()
+            else:
+                rd, ra, _, _, _ = O.cube(pts1, co - co[0], batch.F[s_first * 3:(s_first + 1) * 3], 1)
+                gd = out[:rd.size].cpu().numpy()
+            ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
+            ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
+            parity_ok &= ok
+            n_units += rd.size
+            checked.append(first + s_first)
+        what = "pairs" if wl["mode"] == "pairwise" else "triples"
+        parity = (f"{'bit-exact' if parity_ok else 'MISMATCH'} vs oracle on {len(checked)} scenes "
+                  f"({n_units} {what}, {len(checked)}/{n_slots} allocations; scenes {checked})")
 
     # ---- PCIe-inclusive rate of one launch (never `value`) ------------------
     # the same launch fed from pinned host buffers: H2D of centroids, offsets
@@ -993,6 +1275,9 @@ def main():
     print(json.dumps(out), flush=True)
     if parity_detail and parity_detail["rows_bit_exact"] != parity_detail["rows_checked"]:
         log(f"error: association parity {parity_rows}")
+        raise SystemExit(3)
+    if not parity_ok:
+        log(f"error: residual parity {parity}")
         raise SystemExit(3)
 
 

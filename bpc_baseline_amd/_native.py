@@ -36,7 +36,7 @@ class MvmOptions(ctypes.Structure):
         "cube_kernel", "cube_rows_per_instr", "lsap_wave_max_cols", "lsap_multi_g",
         "lsap_lds_max_cols", "lsap_lds_small_cols", "lsap_mid_max_cols", "lsap_reg_max_cols",
         "lsap_reg_threads", "lsap_mreg_max_cols", "pairwise_row_interleave",
-        "cube_cols_per_lane", "pairwise_xcd_fronts")]
+        "cube_cols_per_lane", "pairwise_xcd_fronts", "lsap_sparse_min_cols")]
 
 
 OPTION_FIELDS = [n for n, _ in MvmOptions._fields_[1:]]
@@ -121,6 +121,10 @@ SIGNATURES = {
         _vp, _i32, _vp, _vp, _i32, _vp, _vp,   # cost, dtype, cost_offs, dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp,            # workspace, bytes, row_ind, col_ind, status
         _i64, _i64, _vp, _vp]),             # long_min, long_max, options (host), stream
+    "mvm_lsap_solve_ex2": (ctypes.c_int, [
+        _vp, _i32, _vp, _vp, _i32, _vp, _vp,
+        _vp, _sz, _vp, _vp, _vp,
+        _i64, _i64, _i64, _vp, _vp]),       # long_min, long_max, short_max, options, stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
         ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id

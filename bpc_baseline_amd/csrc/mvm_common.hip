@@ -69,7 +69,7 @@ int mvm_resolve_options(const mvm_options *in, mvm_options &out) {
 
 extern "C" {
 
-const char *mvm_version(void) { return "mvmatch 0.5.0 gfx950"; }
+const char *mvm_version(void) { return "mvmatch 0.6.0 gfx950"; }
 
 const char *mvm_last_error_string(void) { return g_err; }
 

@@ -30,6 +30,7 @@
 
 #include "mvmatch.h"
 #include "mvm_internal.h"
+#include "mvm_lsap_sparse.h"
 
 #pragma clang fp contract(off)
 
@@ -63,21 +64,30 @@ struct LsapArgs {
                                 // <= kRegMaxShort run in lsap_mreg_kernel, mreg_g workgroups each
     int32_t mreg_slots;         // ... in this many co-resident groups of workgroups
     int32_t mreg_lo, mreg_max_cols, mreg_nr_cap;
+    int32_t sparse_lo;          // > 0: long sides >= this (lsap_sparse_class) are solved by
+                                // the candidate-list kernels (mvm_lsap_sparse.hip)
 };
+
+__device__ __forceinline__ bool in_sparse_class(const LsapArgs &a, int64_t R, int64_t K) {
+    return lsap_sparse_class(a.sparse_lo, a.wave_max_cols, R, K);
+}
 
 // lsap_reg_kernel's class: short sides up to this (its row state is in LDS)
 constexpr int kRegMaxShort = 1024;
 constexpr int kRegMaxCols = 4096;      // 512 threads x 8 columns, or 1024 x 4
+// default lower bound of the candidate-list class (mvm_options.lsap_sparse_min_cols)
+constexpr int kSparseMinCols = 4097;
 
 __device__ __forceinline__ bool in_reg_class(const LsapArgs &a, int64_t R, int64_t K) {
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
     return a.reg_max_cols > 0 && lng > a.wave_max_cols && lng <= a.reg_max_cols &&
-           sht <= kRegMaxShort;
+           sht <= kRegMaxShort && !in_sparse_class(a, R, K);
 }
 
 __device__ __forceinline__ bool in_mreg_class(const LsapArgs &a, int64_t R, int64_t K) {
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
-    return a.mreg_g > 0 && lng > a.mreg_lo && lng <= a.mreg_max_cols && sht > 0 && sht <= kRegMaxShort;
+    return a.mreg_g > 0 && lng > a.mreg_lo && lng <= a.mreg_max_cols && sht > 0 && sht <= kRegMaxShort &&
+           !in_sparse_class(a, R, K);
 }
 
 // Column state of lsap_kernel<.., true> in LDS: spc, v (f64), path, row4col,
@@ -193,6 +203,7 @@ __global__ __launch_bounds__(NT) void lsap_kernel(LsapArgs a) {
     if (a.multi_g > 1) return;                         // solved by lsap_multi_kernel
     if (in_reg_class(a, R, K)) return;                 // solved by lsap_reg_kernel
     if (in_mreg_class(a, R, K)) return;                // solved by lsap_mreg_kernel
+    if (in_sparse_class(a, R, K)) return;              // solved by the candidate-list kernels
     const int64_t longside = R > K ? R : K;
     // class of the problem: LDS state with 256 threads (long side <= lds_small)
     // or 1024 threads, then workspace state with 256 or 1024 threads
@@ -974,6 +985,7 @@ __global__ __launch_bounds__(kLsapThreads) void lsap_multi_kernel(LsapArgs a, in
     const int64_t R = a.dims[2 * p], K = a.dims[2 * p + 1];
     if (R == 0 || K == 0 || (R > K ? R : K) <= a.wave_max_cols) return;
     if (in_mreg_class(a, R, K)) return;                // solved by lsap_mreg_kernel
+    if (in_sparse_class(a, R, K)) return;              // solved by the candidate-list kernels
     const bool transpose = K < R;
     const int64_t nr = transpose ? K : R, nc = transpose ? R : K;
     const int64_t c0 = nc * g / G, c1 = nc * (g + 1) / G;   // owned columns [c0, c1)
@@ -1730,7 +1742,7 @@ timeout:
 // Launch every kernel class of the batch for cost element type CT.
 template <typename CT>
 int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_min,
-                int64_t long_max, const mvm_options &o, hipStream_t s) {
+                int64_t long_max, int64_t short_max, const mvm_options &o, hipStream_t s) {
     // long sides up to wave_max: the one-wave-per-problem kernel (default
     // 1024, -1 = never, capped at 1024)
     int wave_max = o.lsap_wave_max_cols == 0 ? kWaveMaxCols : o.lsap_wave_max_cols;
@@ -1743,11 +1755,32 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
         long_min = long_max = 0;
     }
     auto overlaps = [&](int64_t lo, int64_t hi) { return long_max >= lo && long_min <= hi; };
+    // candidate-list kernels (mvm_lsap_sparse.hip) for wide problems: long
+    // sides >= lsap_sparse_min_cols (default kSparseMinCols), <= 65,536, short
+    // sides <= 1,024.  They also write status 0 for the empty problems.
+    bool empty_done = false, sparse_all = false;
+    {
+        const int sp_lo = o.lsap_sparse_min_cols == 0 ? kSparseMinCols
+                                                      : (o.lsap_sparse_min_cols < 0 ? 0 : o.lsap_sparse_min_cols);
+        const int64_t s_max = short_max < long_max ? short_max : long_max;
+        if (sp_lo > 0 && long_max >= sp_lo && long_max > wave_max && s_max >= 1) {
+            a.sparse_lo = sp_lo;
+            LsapSparseArgs sa{a.cost, a.cost_offs, a.dims, a.ws_offs, a.ws, a.out_offs, a.row_ind,
+                              a.col_ind, a.status, sp_lo, wave_max,
+                              (int32_t)(s_max < kSpMaxShort ? s_max : kSpMaxShort)};
+            const int st = sizeof(CT) == 8 ? lsap_sparse_launch_f64(sa, n_problems, long_max, s)
+                                            : lsap_sparse_launch_f32(sa, n_problems, long_max, s);
+            if (st != MVM_OK) return st;
+            empty_done = true;
+            // every non-empty problem is the class's: no other class has work
+            sparse_all = long_min >= sp_lo && long_min > wave_max && long_max <= kSpMaxCols &&
+                         short_max <= kSpMaxShort;
+        }
+    }
     const dim3 wgrid((unsigned)((n_problems + kWaveProblems - 1) / kWaveProblems));
     const dim3 wblock(64 * kWaveProblems);
-    bool empty_done = false;
     if (wave_max > 0) {
-        if (overlaps(0, 64) || long_max == 0) {
+        if (overlaps(0, 64) || (long_max == 0 && !empty_done)) {
             lsap_wave_kernel<CT, 1><<<wgrid, wblock, 0, s>>>(a, n_problems);
             empty_done = true;
         }
@@ -1776,7 +1809,7 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
             empty_done = true;
         }
     }
-    const bool big = long_max > wave_max;   // anything left for the workgroup kernels
+    const bool big = long_max > wave_max && !sparse_all;   // anything left for the workgroup kernels
     int reg_max = o.lsap_reg_max_cols == 0 ? kRegMaxCols : o.lsap_reg_max_cols;
     reg_max = reg_max < 0 ? 0 : (reg_max > kRegMaxCols ? kRegMaxCols : reg_max);
     a.reg_max_cols = reg_max > wave_max ? reg_max : 0;
@@ -1939,7 +1972,14 @@ int64_t mvm_lsap_plan_ex(int32_t n_problems, const int64_t *rows, const int64_t 
         out_offs[p] = o;
         const bool tr = cols[p] < rows[p];
         const int64_t nr = tr ? cols[p] : rows[p], nc = tr ? rows[p] : cols[p];
-        w += (rows[p] && cols[p]) ? (int64_t)lsap_layout(nr, nc, tr, elem).total : 0;
+        // room for whichever class solves it: the dense layout, or the
+        // candidate lists of the wide class (mvm_lsap_sparse.h)
+        int64_t need = (rows[p] && cols[p]) ? (int64_t)lsap_layout(nr, nc, tr, elem).total : 0;
+        if (rows[p] && cols[p] && nc <= kSpMaxCols && nr <= kSpMaxShort) {
+            const int64_t sp = (int64_t)lsap_sparse_layout(nr, nc, elem).total;
+            need = sp > need ? sp : need;
+        }
+        w += need;
         o += rows[p] < cols[p] ? rows[p] : cols[p];
     }
     ws_offs[n_problems] = w;
@@ -1959,6 +1999,17 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                       int64_t long_min, int64_t long_max, const mvm_options *opts,
                       mvm_stream_t stream) {
+    return mvm_lsap_solve_ex2(cost_dev, cost_dtype, cost_offs_dev, dims_dev, n_problems, ws_offs_dev,
+                              out_offs_dev, workspace_dev, workspace_bytes, row_ind_dev, col_ind_dev,
+                              status_dev, long_min, long_max, long_max, opts, stream);
+}
+
+int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *cost_offs_dev,
+                       const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                       const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                       int64_t long_min, int64_t long_max, int64_t short_max,
+                       const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
     mvm_options o;
     int st = mvm_resolve_options(opts, o);
@@ -1987,11 +2038,11 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
                    ~(uintptr_t)255),   // at or after the per-problem regions (all 256-aligned)
-               0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (cost_dtype == MVM_F64)
-        return lsap_launch<double>(a, n_problems, sync_bytes, long_min, long_max, o, s);
-    return lsap_launch<float>(a, n_problems, sync_bytes, long_min, long_max, o, s);
+        return lsap_launch<double>(a, n_problems, sync_bytes, long_min, long_max, short_max, o, s);
+    return lsap_launch<float>(a, n_problems, sync_bytes, long_min, long_max, short_max, o, s);
 }
 
 int mvm_lsap_solve_bounded(const float *cost_dev, const int64_t *cost_offs_dev,

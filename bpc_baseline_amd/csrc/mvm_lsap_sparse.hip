@@ -1,0 +1,761 @@
+// mvm_lsap_sparse.hip — scipy's assignment for wide problems through candidate lists.
+//
+// Same result as mvm_lsap.hip's kernels (scipy 1.14's shortest augmenting
+// path, oracle/lsap.py), different decomposition, for problems whose long
+// side L (<= 65,536) is much longer than the short side S (<= 1,024): the
+// flattened (N*M, P) cubes of match_objects (epipolar_matching.py:100-116) at
+// tens to hundreds of detections per view.  The dense kernels scan all L
+// columns at every Dijkstra step (65,536 per step at 256 per view, split over
+// 16 workgroups that meet once per step).  Here one workgroup solves a
+// problem alone and a step touches only the assigned columns (at most S) and
+// one short candidate list, because a column no search has assigned yet has
+// v == 0 and an r that is a monotone function of its cost alone (the
+// argument and its model: oracle/lsap_sparse.py, checked against scipy's
+// restatement in tests/test_lsap_sparse_model.py).  Three launches:
+//
+//   sp_blockmin_kernel   every cost entry read once (HBM-bound): the minimum
+//                        of each 32-column block of each short-side row, as
+//                        ordered integer keys; NaN / -inf flag the problem;
+//   sp_lists_kernel      one wave per short-side row: theta = the 16th
+//                        smallest block minimum; the list = every column with
+//                        cost <= theta (>= 16 entries, <= 128, else the row
+//                        is scanned densely when it is needed);
+//   sp_solve_kernel      one 256-thread workgroup per problem: per step the
+//                        assigned columns' costs of the visited row (one
+//                        gather) and the row's list (one load), one block
+//                        reduction, scipy's decision rule.
+#include "mvm_lsap_sparse.h"
+
+#include <math.h>
+#include <stdint.h>
+
+#include "mvm_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kSpNT = 256;
+constexpr int kSpRowGroups = 16;   // sp_lists_kernel workgroups per problem (4 rows each at a time)
+
+template <typename CT>
+struct SpKey;
+template <>
+struct SpKey<float> {
+    using T = uint32_t;
+    static constexpr T kMax = 0xFFFFFFFFu;
+    // order-preserving integer image of a non-NaN float, with -0 taken as +0
+    __device__ static T of(float x) {
+        const uint32_t b = __float_as_uint(x + 0.0f);
+        return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    }
+    __device__ static float val(T k) { return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k); }
+    __device__ static float next_up(float x) { return nextafterf(x, INFINITY); }
+};
+template <>
+struct SpKey<double> {
+    using T = uint64_t;
+    static constexpr T kMax = ~0ull;
+    __device__ static T of(double x) {
+        const uint64_t b = (uint64_t)__double_as_longlong(x + 0.0);
+        return (b >> 63) ? ~b : (b | (1ull << 63));
+    }
+    __device__ static double val(T k) {
+        return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+    }
+    __device__ static double next_up(double x) { return nextafter(x, (double)INFINITY); }
+};
+
+template <typename CT>
+__device__ __forceinline__ bool sp_invalid(CT v) {
+    return (v != v) || (v == -(CT)INFINITY);
+}
+
+// ---- wave / workgroup reductions (DPP row steps, then the four rows) -------
+
+template <int CTRL>
+__device__ __forceinline__ double sp_dpp_f64(double x) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)b, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(b >> 32), (int)(uint32_t)(b >> 32), CTRL,
+                                               0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+
+__device__ __forceinline__ double sp_readlane_f64(double x, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(x);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// minimum over the wave (values are never NaN), uniform
+__device__ __forceinline__ double sp_wave_min(double x) {
+    x = fmin(x, sp_dpp_f64<0xB1>(x));
+    x = fmin(x, sp_dpp_f64<0x4E>(x));
+    x = fmin(x, sp_dpp_f64<0x141>(x));
+    x = fmin(x, sp_dpp_f64<0x140>(x));
+    return fmin(fmin(sp_readlane_f64(x, 0), sp_readlane_f64(x, 16)),
+                fmin(sp_readlane_f64(x, 32), sp_readlane_f64(x, 48)));
+}
+
+template <int CTRL>
+__device__ __forceinline__ int sp_dpp_i32(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ int sp_wave_min_i32(int x) {
+    x = min(x, sp_dpp_i32<0xB1>(x));
+    x = min(x, sp_dpp_i32<0x4E>(x));
+    x = min(x, sp_dpp_i32<0x141>(x));
+    x = min(x, sp_dpp_i32<0x140>(x));
+    return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+               min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+}
+
+__device__ __forceinline__ long long sp_wave_max_i64(long long x) {
+    for (int o = 1; o < 64; o <<= 1) {
+        const long long y = __shfl_xor(x, o);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+
+__device__ __forceinline__ int sp_mbcnt(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// ---- 1. block minima ---------------------------------------------------------
+
+// W[s][j] (short-side row s, long-side column j) of a problem
+template <typename CT>
+__device__ __forceinline__ CT sp_w(const CT *C0, bool tr, int S, int L, int s, int j) {
+    return tr ? C0[(int64_t)j * S + s] : C0[(int64_t)s * L + j];
+}
+
+template <typename CT>
+__global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, int32_t n, int32_t tpp) {
+    using K = SpKey<CT>;
+    using KT = typename K::T;
+    constexpr int kKeys = 65536 / (int)sizeof(KT);         // 64 KiB of LDS keys per pass
+    constexpr int VW = 16 / (int)sizeof(CT);               // elements per 16-byte load
+    __shared__ KT s_key[kKeys];
+    const int p = (int)(blockIdx.x / (unsigned)tpp), w = (int)(blockIdx.x % (unsigned)tpp);
+    if (p >= n) return;
+    const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
+    const bool tr = Kd < R;
+    const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
+    const int j0 = w * kSpTileCols;
+    if (j0 >= L) return;
+    const int j1 = min(j0 + kSpTileCols, L);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    unsigned char *ws = a.ws + a.ws_offs[p];
+    KT *bm = reinterpret_cast<KT *>(ws + y.bm);
+    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
+    const int nb = (L + kSpBlock - 1) / kSpBlock;
+    int bp = 64;                                           // blocks per LDS pass
+    while (bp > 1 && S * bp > kKeys) bp >>= 1;
+    const int t = threadIdx.x;
+    const int G = S / VW;                                  // 16-byte groups per tall row
+    // tall input, whole 16-byte groups, 16-byte aligned, and a group count that
+    // divides the workgroup: every thread keeps one group's running minima
+    const bool fast = tr && S % VW == 0 && kSpNT % G == 0 &&
+                      ((reinterpret_cast<uintptr_t>(C0)) & 15) == 0;
+    int bad = 0;
+    for (int pj0 = j0; pj0 < j1; pj0 += bp * kSpBlock) {
+        const int pj1 = min(pj0 + bp * kSpBlock, j1), nbk = (pj1 - pj0 + kSpBlock - 1) / kSpBlock;
+        for (int x = t; x < S * bp; x += kSpNT) s_key[x] = K::kMax;
+        __syncthreads();
+        if (fast) {
+            const int q = kSpNT / G, g = t % G, r0 = t / G, nr = pj1 - pj0;
+            KT run[VW];
+#pragma unroll
+            for (int v = 0; v < VW; ++v) run[v] = K::kMax;
+            int cur = r0 >> 5;
+            for (int r = r0; r < nr; r += q) {
+                const int blk = r >> 5;
+                if (blk != cur) {
+#pragma unroll
+                    for (int v = 0; v < VW; ++v) {
+                        atomicMin(&s_key[(g * VW + v) * bp + cur], run[v]);
+                        run[v] = K::kMax;
+                    }
+                    cur = blk;
+                }
+                CT val[VW];
+                *reinterpret_cast<uint4 *>(val) =
+                    *reinterpret_cast<const uint4 *>(C0 + (int64_t)(pj0 + r) * S + g * VW);
+#pragma unroll
+                for (int v = 0; v < VW; ++v) {
+                    bad |= sp_invalid(val[v]);
+                    const KT kk = K::of(val[v]);
+                    run[v] = kk < run[v] ? kk : run[v];
+                }
+            }
+            if (r0 < nr) {
+#pragma unroll
+                for (int v = 0; v < VW; ++v) atomicMin(&s_key[(g * VW + v) * bp + cur], run[v]);
+            }
+        } else {
+            // any layout: one element per thread and step, (row, column) stepped
+            // incrementally (no division in the loop)
+            const int W = pj1 - pj0;
+            const int64_t total = (int64_t)S * W;
+            if (tr) {                                      // element e: tall row e / S, s = e % S
+                int r = t / S, s = t % S;
+                const int dq = kSpNT / S, dr = kSpNT % S;
+                for (int64_t e = t; e < total; e += kSpNT) {
+                    const CT v = C0[(int64_t)(pj0 + r) * S + s];
+                    bad |= sp_invalid(v);
+                    atomicMin(&s_key[s * bp + (r >> 5)], K::of(v));
+                    r += dq;
+                    s += dr;
+                    if (s >= S) {
+                        s -= S;
+                        ++r;
+                    }
+                }
+            } else {                                       // element e: s = e / W, column e % W
+                int s = t / W, jj = t % W;
+                const int dq = kSpNT / W, dr = kSpNT % W;
+                for (int64_t e = t; e < total; e += kSpNT) {
+                    const CT v = C0[(int64_t)s * L + pj0 + jj];
+                    bad |= sp_invalid(v);
+                    atomicMin(&s_key[s * bp + (jj >> 5)], K::of(v));
+                    s += dq;
+                    jj += dr;
+                    if (jj >= W) {
+                        jj -= W;
+                        ++s;
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        for (int x = t; x < S * nbk; x += kSpNT) {
+            const int s = x / nbk, bb = x - s * nbk;
+            bm[(int64_t)s * nb + (pj0 / kSpBlock) + bb] = s_key[s * bp + bb];
+        }
+        __syncthreads();
+    }
+    bad = __syncthreads_or(bad);
+    if (t == 0) reinterpret_cast<int32_t *>(ws + y.flags)[w] = bad;
+}
+
+// ---- 2. candidate lists --------------------------------------------------------
+
+template <typename CT>
+__global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32_t n) {
+    using K = SpKey<CT>;
+    using KT = typename K::T;
+    constexpr int kQ = kSpMaxCols / kSpBlock / 64;         // block keys per lane (32)
+    __shared__ int32_t s_cand[kSpNT / 64][kSpLCap];
+    const int p = (int)(blockIdx.x / kSpRowGroups), grp = (int)(blockIdx.x % kSpRowGroups);
+    if (p >= n) return;
+    const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
+    const bool tr = Kd < R;
+    const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    unsigned char *ws = a.ws + a.ws_offs[p];
+    const KT *bm = reinterpret_cast<const KT *>(ws + y.bm);
+    int32_t *lcol = reinterpret_cast<int32_t *>(ws + y.lcol);
+    CT *lval = reinterpret_cast<CT *>(ws + y.lval);
+    int32_t *ln = reinterpret_cast<int32_t *>(ws + y.ln);
+    CT *theta_out = reinterpret_cast<CT *>(ws + y.theta);
+    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
+    const int nb = (L + kSpBlock - 1) / kSpBlock;
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    for (int s = grp * (kSpNT / 64) + wave; s < S; s += kSpRowGroups * (kSpNT / 64)) {
+        KT k[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const int idx = lane + 64 * q;
+            k[q] = idx < nb ? bm[(int64_t)s * nb + idx] : K::kMax;
+        }
+        KT thr = K::kMax;
+        CT theta = (CT)INFINITY;
+        if (nb > kSpTB) {                                  // the kSpTB-th smallest key
+            KT lo = 0, hi = K::kMax;
+            while (lo < hi) {
+                const KT mid = lo + (hi - lo) / 2;
+                int cnt = 0;
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) cnt += __popcll(__ballot(k[q] <= mid));
+                if (cnt >= kSpTB) hi = mid;
+                else lo = mid + 1;
+            }
+            thr = lo;
+            theta = K::val(thr);
+        }
+        int ncand = 0;                                     // candidate blocks (uniform)
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+            const bool c = k[q] <= thr && lane + 64 * q < nb;
+            const uint64_t m = __ballot(c);
+            if (c) {
+                const int pos = ncand + sp_mbcnt(m);
+                if (pos < kSpLCap) s_cand[wave][pos] = lane + 64 * q;
+            }
+            ncand += __popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        int cnt = kSpLCap + 1;                             // every candidate block holds an entry
+        if (ncand <= kSpLCap) {
+            cnt = 0;
+            for (int m0 = 0; m0 < ncand; m0 += 16) {       // two blocks per load, 8 loads in flight
+                CT val[8];
+                int col[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int idx = m0 + 2 * u + (lane >> 5);
+                    const int blk = idx < ncand ? s_cand[wave][idx] : -1;
+                    const int j = blk * kSpBlock + (lane & 31);
+                    col[u] = (blk >= 0 && j < L) ? j : -1;
+                    val[u] = col[u] >= 0 ? sp_w(C0, tr, S, L, s, j) : (CT)0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const bool keep = col[u] >= 0 && val[u] <= theta;
+                    const uint64_t m = __ballot(keep);
+                    if (keep) {
+                        const int pos = cnt + sp_mbcnt(m);
+                        if (pos < kSpLCap) {
+                            lcol[(int64_t)s * kSpLCap + pos] = col[u];
+                            lval[(int64_t)s * kSpLCap + pos] = val[u];
+                        }
+                    }
+                    cnt += __popcll(m);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+            ln[s] = cnt <= kSpLCap ? cnt : -1;
+            theta_out[s] = theta;
+        }
+    }
+}
+
+// ---- 3. the solver ------------------------------------------------------------
+
+struct SpRec {
+    double a;          // smallest shortest-path cost over the wave's assigned columns
+    double f;          // smallest r over the wave's free list entries
+    int32_t a_pos;     // scan position of the first assigned column holding a
+    int32_t a_q;       // its slot (-1: none)
+    int32_t a_ps;      // its path step
+    int32_t f_any;     // some list entry of the wave is free
+    int32_t tail_q;    // the slot at scan position n_rem - 1 (-1: none in this wave)
+    int32_t pad;
+};
+
+// dynamic LDS of sp_solve_kernel: bitmaps of lw words, row and step arrays of cap
+__host__ __device__ inline size_t sp_solve_lds_bytes(int lw, int cap) {
+    return (size_t)2 * lw * 4 + (size_t)8 * (cap + 4 * (cap + 1)) + (size_t)4 * (3 * cap + 5 * (cap + 1));
+}
+
+template <typename CT>
+__device__ __forceinline__ double sp_block_min(double x, double *s_red, int wave) {
+    x = sp_wave_min(x);
+    if ((threadIdx.x & 63) == 0) s_red[wave] = x;
+    __syncthreads();
+    const double r = fmin(fmin(s_red[0], s_red[1]), fmin(s_red[2], s_red[3]));
+    __syncthreads();
+    return r;
+}
+
+__device__ __forceinline__ long long sp_block_max_i64(long long x, long long *s_red, int wave) {
+    x = sp_wave_max_i64(x);
+    if ((threadIdx.x & 63) == 0) s_red[wave] = x;
+    __syncthreads();
+    long long r = s_red[0];
+    for (int w = 1; w < kSpNT / 64; ++w) r = s_red[w] > r ? s_red[w] : r;
+    __syncthreads();
+    return r;
+}
+
+template <typename CT, int KS>
+__global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32_t n, int32_t lw) {
+    __shared__ SpRec s_rec[2][kSpNT / 64];
+    __shared__ double s_redd[kSpNT / 64];
+    __shared__ long long s_redl[kSpNT / 64];
+    extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+    const int p = blockIdx.x;
+    if (p >= n) return;
+    const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+    if (R == 0 || Kd == 0) {                                 // scipy: an empty assignment
+        if (threadIdx.x == 0) a.status[p] = 0;
+        return;
+    }
+    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
+    const bool tr = Kd < R;
+    const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
+    const int cap = a.s_cap;
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    const unsigned char *ws = a.ws + a.ws_offs[p];
+    const int32_t *lcol = reinterpret_cast<const int32_t *>(ws + y.lcol);
+    const CT *lval = reinterpret_cast<const CT *>(ws + y.lval);
+    const int32_t *ln = reinterpret_cast<const int32_t *>(ws + y.ln);
+    const CT *theta = reinterpret_cast<const CT *>(ws + y.theta);
+    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+
+    uint32_t *s_asg = reinterpret_cast<uint32_t *>(s_dyn);   // [lw] assigned columns
+    uint32_t *s_mvb = s_asg + lw;                             // [lw] free columns moved this search
+    double *s_u = reinterpret_cast<double *>(s_mvb + lw);     // [cap] row duals
+    double *s_m = s_u + cap;                                  // [cap+1] step minimum
+    double *s_mp = s_m + cap + 1;                             // [cap+1] minVal of the step's scan
+    double *s_f = s_mp + cap + 1;                             // [cap+1] free minimum of the step's row
+    double *s_rb = s_f + cap + 1;                             // [cap+1] r at beta (NaN: scan densely)
+    int32_t *s_c4r = reinterpret_cast<int32_t *>(s_rb + cap + 1);   // [cap] row -> slot
+    int32_t *s_r4c = s_c4r + cap;                             // [cap] slot -> row
+    int32_t *s_col = s_r4c + cap;                             // [cap] slot -> column
+    int32_t *s_i = s_col + cap;                               // [cap+1] step row
+    int32_t *s_sl = s_i + cap + 1;                            // [cap+1] step's chosen slot
+    int32_t *s_ps = s_sl + cap + 1;                           // [cap+1] its path step
+    int32_t *s_mvc = s_ps + cap + 1;                          // [cap+1] moved free column
+    int32_t *s_mvp = s_mvc + cap + 1;                         // [cap+1] ... its scan position
+
+    // NaN / -inf anywhere (sp_blockmin_kernel's tile flags): scipy's ValueError
+    {
+        const int nt = (L + kSpTileCols - 1) / kSpTileCols;
+        const int32_t *fl = reinterpret_cast<const int32_t *>(ws + y.flags);
+        int bad = 0;
+        for (int x = t; x < nt; x += kSpNT) bad |= fl[x];
+        if (__syncthreads_or(bad)) {
+            if (t == 0) a.status[p] = 1;
+            return;
+        }
+    }
+    for (int x = t; x < lw; x += kSpNT) {
+        s_asg[x] = 0u;
+        s_mvb[x] = 0u;
+    }
+    for (int x = t; x < S; x += kSpNT) {
+        s_u[x] = 0.0;
+        s_c4r[x] = -1;
+    }
+    // slot state: slot q = t + 256 m lives in thread t's registers
+    double v[KS], spc[KS];
+    int32_t col[KS], pos[KS], ps[KS];
+    uint32_t rem = 0;                                         // bit m: slot removed this search
+#pragma unroll
+    for (int m = 0; m < KS; ++m) {
+        v[m] = 0.0;
+        col[m] = -1;
+    }
+    __syncthreads();
+    auto asg = [&](int j) { return (s_asg[j >> 5] >> (j & 31)) & 1u; };
+    auto mvd = [&](int j) { return (s_mvb[j >> 5] >> (j & 31)) & 1u; };
+    auto rfree = [](double mp, CT c, double ui) { return ((mp + (double)c) - ui) - 0.0; };
+
+    int par = 0;
+    for (int cur = 0; cur < S; ++cur) {
+        const int na = cur;                                   // slots 0 .. na-1 are assigned columns
+#pragma unroll
+        for (int m = 0; m < KS; ++m) {
+            spc[m] = INFINITY;
+            ps[m] = -1;
+            pos[m] = L - 1 - col[m];
+        }
+        rem = 0;
+        int i = cur, k = 0, n_rem = L, n_mv = 0;
+        double m_prev = 0.0, F = INFINITY, lowest = INFINITY;
+        int sink = -1, sink_ps = -1;
+        while (true) {
+            // ---- one Dijkstra step: every load of the step in flight at once
+            const double ui = s_u[i];
+            const int nl = ln[i];
+            const CT th = theta[i];
+            CT cv[KS];
+#pragma unroll
+            for (int m = 0; m < KS; ++m) {
+                const int q = t + kSpNT * m;
+                cv[m] = (q < na && !((rem >> m) & 1u)) ? sp_w(C0, tr, S, L, i, col[m]) : (CT)0;
+            }
+            int lc = 0;
+            CT lv = (CT)0;
+            if (t < kSpLCap) {
+                lc = lcol[(int64_t)i * kSpLCap + t];
+                lv = lval[(int64_t)i * kSpLCap + t];
+            }
+            double ba = INFINITY;
+            int bpos = 0x7FFFFFFF, bq = -1, bps = -1, tq = -1;
+#pragma unroll
+            for (int m = 0; m < KS; ++m) {
+                const int q = t + kSpNT * m;
+                if (q < na && !((rem >> m) & 1u)) {
+                    const double r = ((m_prev + (double)cv[m]) - ui) - v[m];
+                    if (r < spc[m]) {
+                        spc[m] = r;
+                        ps[m] = k;
+                    }
+                    if (spc[m] < ba || (spc[m] == ba && pos[m] < bpos)) {
+                        ba = spc[m];
+                        bpos = pos[m];
+                        bq = q;
+                        bps = ps[m];
+                    }
+                    if (pos[m] == n_rem - 1) tq = q;
+                }
+            }
+            double fr = INFINITY;
+            int fany = 0;
+            if (t < kSpLCap && t < nl && !asg(lc)) {
+                fr = rfree(m_prev, lv, ui);
+                fany = 1;
+            }
+            // wave records
+            {
+                const double wa = sp_wave_min(ba);
+                const bool el = bq >= 0 && ba == wa;
+                const int wpos = sp_wave_min_i32(el ? bpos : 0x7FFFFFFF);
+                const uint64_t win = __ballot(el && bpos == wpos);
+                const int wl = win ? (int)__builtin_ctzll(win) : 0;
+                const int wq = win ? __builtin_amdgcn_readlane(bq, wl) : -1;
+                const int wps = win ? __builtin_amdgcn_readlane(bps, wl) : -1;
+                const double wf = sp_wave_min(fr);
+                const uint64_t fa = __ballot(fany);
+                const uint64_t tm = __ballot(tq >= 0);
+                const int wt = tm ? __builtin_amdgcn_readlane(tq, (int)__builtin_ctzll(tm)) : -1;
+                if (lane == 0) s_rec[par][wave] = SpRec{wa, wf, wpos, wq, wps, fa != 0, wt, 0};
+            }
+            __syncthreads();
+            double A = INFINITY, fk = INFINITY;
+            int apos = 0x7FFFFFFF, aq = -1, aps = -1, f_any = 0, tail_q = -1;
+#pragma unroll
+            for (int w = 0; w < kSpNT / 64; ++w) {
+                const SpRec r = s_rec[par][w];
+                if (r.a_q >= 0 && (r.a < A || (r.a == A && r.a_pos < apos))) {
+                    A = r.a;
+                    apos = r.a_pos;
+                    aq = r.a_q;
+                    aps = r.a_ps;
+                }
+                fk = fmin(fk, r.f);
+                f_any |= r.f_any;
+                tail_q = r.tail_q >= 0 ? r.tail_q : tail_q;
+            }
+            par ^= 1;
+            double rb;
+            if (nl < 0 || !f_any) {
+                // no free list entry (or no list): the row's free minimum densely
+                double d = INFINITY;
+                for (int j0 = t; j0 < L; j0 += kSpNT * 8) {
+                    CT c[8];
+                    bool ok[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int j = j0 + kSpNT * u;
+                        ok[u] = j < L && !asg(j);
+                        c[u] = ok[u] ? sp_w(C0, tr, S, L, i, j) : (CT)0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (ok[u]) d = fmin(d, rfree(m_prev, c[u], ui));
+                }
+                fk = sp_block_min<CT>(d, s_redd, wave);
+                rb = NAN;                                     // ties need the dense scan too
+            } else {
+                rb = isinf(th) ? (double)INFINITY : rfree(m_prev, SpKey<CT>::next_up(th), ui);
+            }
+            if (t == 0) {
+                s_i[k] = i;
+                s_mp[k] = m_prev;
+                s_f[k] = fk;
+                s_rb[k] = rb;
+            }
+            F = fmin(F, fk);
+            lowest = fmin(A, F);
+            if (!(lowest < INFINITY)) break;                  // infeasible
+            if (!(A < F)) {
+                // a free column reaches the minimum: the one latest in scan
+                // order among every visited row's free ties is the sink
+                __syncthreads();                              // s_f / s_rb / moved list of this search
+                long long best = -1;
+                for (int s = 0; s <= k; ++s) {
+                    if (s_f[s] != lowest) continue;
+                    const int is = s_i[s];
+                    const double mp = s_mp[s], us = s_u[is], rbs = s_rb[s];
+                    const int nls = ln[is];
+                    const bool dense = nls < 0 || rbs != rbs || rbs == lowest;
+                    long long key = -1;
+                    if (!dense) {
+                        if (t < nls) {
+                            const int c = lcol[(int64_t)is * kSpLCap + t];
+                            if (!asg(c) && !mvd(c) && rfree(mp, lval[(int64_t)is * kSpLCap + t], us) == lowest)
+                                key = ((long long)(L - 1 - c) << 16) | c;
+                        }
+                    } else {
+                        for (int j0 = t; j0 < L; j0 += kSpNT * 8) {
+                            CT c[8];
+                            bool ok[8];
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int j = j0 + kSpNT * u;
+                                ok[u] = j < L && !asg(j) && !mvd(j);
+                                c[u] = ok[u] ? sp_w(C0, tr, S, L, is, j) : (CT)0;
+                            }
+#pragma unroll
+                            for (int u = 0; u < 8; ++u) {
+                                const int j = j0 + kSpNT * u;
+                                if (ok[u] && rfree(mp, c[u], us) == lowest) {
+                                    const long long kk = ((long long)(L - 1 - j) << 16) | j;
+                                    key = kk > key ? kk : key;
+                                }
+                            }
+                        }
+                    }
+                    for (int mm = t; mm < n_mv; mm += kSpNT) {   // free columns off their default place
+                        const int c = s_mvc[mm];
+                        if (rfree(mp, sp_w(C0, tr, S, L, is, c), us) == lowest) {
+                            const long long kk = ((long long)s_mvp[mm] << 16) | c;
+                            key = kk > key ? kk : key;
+                        }
+                    }
+                    key = sp_block_max_i64(key, s_redl, wave);
+                    if (key > best) {                         // the first row reaching it is its path
+                        best = key;
+                        sink_ps = s;
+                    }
+                }
+                sink = (int)(best & 0xFFFF);
+                if (t == 0) {
+                    s_m[k] = lowest;
+                    s_sl[k] = -1;
+                    s_ps[k] = sink_ps;
+                }
+                break;
+            }
+            // an assigned column is the minimum: remove it (swap-with-last) and
+            // continue from its row
+            const int last = n_rem - 1;
+            if (apos != last) {
+                if (tail_q >= 0) {                            // an assigned column sits at the tail
+#pragma unroll
+                    for (int m = 0; m < KS; ++m)
+                        if (t + kSpNT * m == tail_q) pos[m] = apos;
+                } else {
+                    int hit = -1;                             // a moved free column at the tail?
+                    for (int mm = lane; mm < n_mv; mm += 64) {
+                        const uint64_t b = __ballot(s_mvp[mm] == last);
+                        if (b) hit = mm - lane + (int)__builtin_ctzll(b);
+                    }
+                    hit = __builtin_amdgcn_readfirstlane(hit);
+                    if (t == 0) {
+                        if (hit >= 0) {
+                            s_mvp[hit] = apos;
+                        } else {                              // the column at its default place
+                            const int c = L - 1 - last;
+                            s_mvc[n_mv] = c;
+                            s_mvp[n_mv] = apos;
+                            s_mvb[c >> 5] |= 1u << (c & 31);
+                        }
+                    }
+                    if (hit < 0) ++n_mv;
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < KS; ++m)
+                if (t + kSpNT * m == aq) rem |= 1u << m;
+            if (t == 0) {
+                s_m[k] = lowest;
+                s_sl[k] = aq;
+                s_ps[k] = aps;
+            }
+            --n_rem;
+            m_prev = lowest;
+            i = s_r4c[aq];
+            if (++k > S) {                                    // cannot happen: each step removes a slot
+                if (t == 0) a.status[p] = 3;
+                return;
+            }
+        }
+        if (sink < 0) {                                       // infeasible: scipy's ValueError
+            if (t == 0) a.status[p] = 2;
+            return;
+        }
+        // ---- duals, the new assigned column, the augmenting path
+        if (t == 0) s_u[cur] += lowest;
+        for (int tt = 1 + t; tt <= k; tt += kSpNT) s_u[s_i[tt]] += lowest - s_m[tt - 1];
+#pragma unroll
+        for (int m = 0; m < KS; ++m) {
+            if ((rem >> m) & 1u) v[m] -= lowest - spc[m];
+            if (t + kSpNT * m == na) {                       // slot na: the sink, v stays 0
+                col[m] = sink;
+                v[m] = 0.0;
+            }
+        }
+        for (int mm = t; mm < n_mv; mm += kSpNT) {
+            const int c = s_mvc[mm];
+            atomicAnd(&s_mvb[c >> 5], ~(1u << (c & 31)));
+        }
+        if (t == 0) {
+            s_col[na] = sink;
+            s_asg[sink >> 5] |= 1u << (sink & 31);
+            int kk = k;
+            while (true) {                                    // path[j_kk] = i_(its path step)
+                const int s = s_ps[kk], i2 = s_i[s];
+                const int q = kk == k ? na : s_sl[kk];
+                s_c4r[i2] = q;
+                s_r4c[q] = i2;
+                if (s == 0) break;
+                kk = s - 1;
+            }
+        }
+        __syncthreads();
+    }
+    // ---- output in scipy's order
+    const int64_t o = a.out_offs[p];
+    if (tr) {
+        for (int kk = t; kk < S; kk += kSpNT) {
+            const int rk = s_col[s_c4r[kk]];
+            int rank = 0;
+            for (int k2 = 0; k2 < S; ++k2) rank += s_col[s_c4r[k2]] < rk;
+            a.row_ind[o + rank] = rk;
+            a.col_ind[o + rank] = kk;
+        }
+    } else {
+        for (int kk = t; kk < S; kk += kSpNT) {
+            a.row_ind[o + kk] = kk;
+            a.col_ind[o + kk] = s_col[s_c4r[kk]];
+        }
+    }
+    if (t == 0) a.status[p] = 0;
+}
+
+template <typename CT>
+int sp_launch(const LsapSparseArgs &a0, int32_t n, int64_t long_max, hipStream_t s) {
+    LsapSparseArgs a = a0;
+    const int64_t lmax = long_max < kSpMaxCols ? long_max : kSpMaxCols;
+    const int tpp = (int)((lmax + kSpTileCols - 1) / kSpTileCols);
+    if ((int64_t)n * tpp * kSpNT > 0xFFFFFFFFLL || (int64_t)n * kSpRowGroups * kSpNT > 0xFFFFFFFFLL)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "%d problems in one batch: split it", (int)n);
+    sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
+    sp_lists_kernel<CT><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
+    const int cap = a.s_cap;
+    const int lw = (int)(((lmax + 63) / 64) * 2);            // even: the f64 arrays stay 8-aligned
+    const size_t lds = sp_solve_lds_bytes(lw, cap);
+    const void *kern = cap <= kSpNT ? reinterpret_cast<const void *>(&sp_solve_kernel<CT, 1>)
+                                    : reinterpret_cast<const void *>(&sp_solve_kernel<CT, 4>);
+    if (lds > 64 * 1024 && hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)lds) != hipSuccess)
+        return mvm_fail(MVM_ERR_HIP, "cannot raise the dynamic LDS limit to %zu bytes", lds);
+    if (cap <= kSpNT)
+        sp_solve_kernel<CT, 1><<<dim3((unsigned)n), dim3(kSpNT), lds, s>>>(a, n, lw);
+    else
+        sp_solve_kernel<CT, 4><<<dim3((unsigned)n), dim3(kSpNT), lds, s>>>(a, n, lw);
+    return mvm_check_launch("lsap_sparse");
+}
+
+}  // namespace
+
+int lsap_sparse_launch_f32(const LsapSparseArgs &a, int32_t n, int64_t long_max, hipStream_t s) {
+    return sp_launch<float>(a, n, long_max, s);
+}
+
+int lsap_sparse_launch_f64(const LsapSparseArgs &a, int32_t n, int64_t long_max, hipStream_t s) {
+    return sp_launch<double>(a, n, long_max, s);
+}

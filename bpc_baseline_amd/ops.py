@@ -185,7 +185,7 @@ def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minv
 def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
                    out_offs: Tensor, workspace: Tensor, row_ind: Tensor, col_ind: Tensor,
                    status: Tensor, long_min: int = 1, long_max: int = 2 ** 62,
-                   opts: Optional[List[int]] = None) -> None:
+                   opts: Optional[List[int]] = None, short_max: int = -1) -> None:
     dev = cost.device
     if dev.type != "cuda":
         raise ValueError("cost must be a GPU tensor (the matcher has no CPU path)")
@@ -199,16 +199,17 @@ def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tenso
         _require(t, n, dt, dev)
     n = status.numel()
     dtype = _native.MVM_F64 if cost.dtype == torch.float64 else _native.MVM_F32
-    st = _native.load().mvm_lsap_solve_ex(_p(cost), dtype, _p(cost_offs), _p(dims), n, _p(ws_offs),
-                                          _p(out_offs), _p(workspace), workspace.numel(),
-                                          _p(row_ind), _p(col_ind), _p(status), long_min,
-                                          long_max, _opts_ref(opts), _stream(cost))
-    _native.check("mvm_lsap_solve_ex", st)
+    st = _native.load().mvm_lsap_solve_ex2(_p(cost), dtype, _p(cost_offs), _p(dims), n, _p(ws_offs),
+                                           _p(out_offs), _p(workspace), workspace.numel(),
+                                           _p(row_ind), _p(col_ind), _p(status), long_min,
+                                           long_max, long_max if short_max < 0 else short_max,
+                                           _opts_ref(opts), _stream(cost))
+    _native.check("mvm_lsap_solve_ex2", st)
 
 
 @lsap_solve_out.register_fake
 def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, long_min=1,
-      long_max=2 ** 62, opts=None):
+      long_max=2 ** 62, opts=None, short_max=-1):
     return None
 
 
@@ -504,6 +505,8 @@ class LsapPlan:
         longs = np.maximum(rows, cols)[(rows > 0) & (cols > 0)]
         self.long_min = int(longs.min()) if longs.size else 0     # bounds for the launch
         self.long_max = int(longs.max()) if longs.size else 0
+        shorts = np.minimum(rows, cols)[(rows > 0) & (cols > 0)]
+        self.short_max = int(shorts.max()) if shorts.size else 0
 
 
 def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan, *,
@@ -519,7 +522,7 @@ def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPla
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
                                      plan.workspace, row_ind, col_ind, status, plan.long_min,
-                                     plan.long_max, _opts_list(options))
+                                     plan.long_max, _opts_list(options), plan.short_max)
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
 
 

@@ -129,7 +129,7 @@ class SceneBatch:
     n_scenes: int
     n_cams: int
     seed: int = 0
-    meta: dict = field(default_factory=dict)
+    meta: dict = field(default_factory=dict)   # also the rig: Ks f32 [S,C,3,3], RTs f64 [S,C,4,4]
 
     @property
     def n_pairs(self) -> int:
@@ -175,7 +175,8 @@ def make_scenes(n_scenes: int, n_cams: int, n_dets, *, seed: int = 0, first_scen
     return SceneBatch(pts=np.ascontiguousarray(pts), cam_offs=cam_offs,
                       F=np.ascontiguousarray(F), pairs=np.asarray(pairs, np.int32),
                       n_scenes=n_scenes, n_cams=n_cams, seed=seed,
-                      meta={"first_scene": first_scene, "n_dets": n_dets, "ragged": ragged})
+                      meta={"first_scene": first_scene, "n_dets": n_dets, "ragged": ragged,
+                            "Ks": K_all, "RTs": RT_all})
 
 
 @dataclass

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 5
+#define MVM_ABI_VERSION 6
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -131,6 +131,10 @@ typedef struct mvm_options {
                                        matrices, else 1); 1..16: each XCD writes its
                                        eighth of the grid as this many concurrent
                                        contiguous ranges (ABI 5) */
+    int32_t lsap_sparse_min_cols;   /* 0 default (4097); -1 off: problems with a long
+                                       side >= this (and > the one-wave limit, <= 65536)
+                                       and a short side <= 1024 are solved one workgroup
+                                       each through per-row candidate lists (ABI 6) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */
@@ -272,6 +276,17 @@ int mvm_lsap_solve_ex(const void *cost_dev, int32_t cost_dtype, const int64_t *c
                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                       int64_t long_min, int64_t long_max, const mvm_options *opts,
                       mvm_stream_t stream);
+/*
+ * ... with a host-known bound on min(rows, cols) as well (ABI 6): it sizes the
+ * candidate-list kernels' LDS (a workgroup per problem holds state for every
+ * short-side row).  mvm_lsap_solve_ex passes short_max = long_max.
+ */
+int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *cost_offs_dev,
+                       const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                       const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                       int64_t long_min, int64_t long_max, int64_t short_max,
+                       const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * On-device detection packing, replacing the per-box loop of

@@ -25,7 +25,7 @@ def _batched(cuda, mats, options=None, dtype=np.float32):
 
 
 @pytest.fixture(params=["default", "reg", "reg1024", "mreg", "lds", "workgroup", "workgroup256", "multi",
-                        "nomreg"])
+                        "nomreg", "sparse", "sparse_lo"])
 def lsap_path(request):
     """mvm_options of each assignment kernel class.  default: long sides <=
     1024 one problem per wave, up to 4096 (short sides <= 1024) one workgroup
@@ -39,16 +39,26 @@ def lsap_path(request):
     with a short side <= 1024 in the register-state kernel spread over
     ceil(long / 4096) workgroups (the default above 4096 columns), small
     ones included; nomreg: the default without it (long sides above 4096 in
-    the split / LDS / workspace kernels)."""
-    off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_mreg_max_cols": -1}
+    the split / LDS / workspace kernels); sparse: every problem with a short
+    side <= 1024 and a long side <= 65536 through the candidate-list kernels
+    (the default above 4096 columns: mvm_lsap_sparse.hip), small ones (whose
+    rows are all scanned densely) included; sparse_lo: the same from long
+    sides of 1025 on (lists and dense rows side by side).  Every other path
+    turns the candidate-list class off."""
+    off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_mreg_max_cols": -1,
+           "lsap_sparse_min_cols": -1}
     noreg = dict(off, lsap_reg_max_cols=-1)
     return {"default": None, "reg": off, "reg1024": dict(off, lsap_reg_threads=1024),
-            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1},
+            "mreg": {"lsap_wave_max_cols": -1, "lsap_reg_max_cols": -1, "lsap_multi_g": -1,
+                     "lsap_sparse_min_cols": -1},
             "lds": noreg,
             "workgroup": dict(noreg, lsap_lds_max_cols=-1),
             "workgroup256": dict(noreg, lsap_lds_max_cols=-1, lsap_mid_max_cols=1000000),
-            "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4, "lsap_mreg_max_cols": -1},
-            "nomreg": {"lsap_mreg_max_cols": -1}}[request.param]
+            "multi": {"lsap_wave_max_cols": -1, "lsap_multi_g": 4, "lsap_mreg_max_cols": -1,
+                      "lsap_sparse_min_cols": -1},
+            "nomreg": {"lsap_mreg_max_cols": -1, "lsap_sparse_min_cols": -1},
+            "sparse": {"lsap_wave_max_cols": -1, "lsap_sparse_min_cols": 1},
+            "sparse_lo": {"lsap_sparse_min_cols": 1025}}[request.param]
 
 
 def test_random_shapes_and_ties_batched(cuda, lsap_path):
@@ -175,20 +185,46 @@ def test_register_split_class_edges(cuda, lsap_path):
         assert np.array_equal(r, r0) and np.array_equal(c, c0)
 
 
-@pytest.mark.parametrize("multi_g", [0, -1, 16])
-def test_full_256_cube_equals_scipy(cuda, multi_g):
+@pytest.mark.parametrize("path", ["default", "mreg", "one_workgroup", "multi16"])
+def test_full_256_cube_equals_scipy(cuda, path):
     """Config-2 scale: the (65536 x 256) flattened 256^3 cube of one scene
-    (default: the split register-state kernel; one workgroup; sixteen
-    workgroups of the split workspace-state kernel)."""
+    (default: the candidate-list kernels; the split register-state kernel;
+    one workgroup; sixteen workgroups of the split workspace-state kernel)."""
     from bpc_baseline_amd.synth import make_scenes
     from oracle import oracle as O
     b = make_scenes(1, 3, 256, seed=42)
     cube, _, _, _, _ = O.cube(b.pts, b.cam_offs, b.F, 1)
     flat = cube.reshape(256 * 256, 256)
     r0, c0 = scipy_lsa(flat)
-    opts = {"lsap_multi_g": multi_g} if multi_g == 0 else {"lsap_multi_g": multi_g, "lsap_mreg_max_cols": -1}
+    opts = {"default": None, "mreg": {"lsap_sparse_min_cols": -1},
+            "one_workgroup": {"lsap_multi_g": -1, "lsap_mreg_max_cols": -1, "lsap_sparse_min_cols": -1},
+            "multi16": {"lsap_multi_g": 16, "lsap_mreg_max_cols": -1, "lsap_sparse_min_cols": -1}}[path]
     r1, c1, st = _batched(cuda, [flat], opts)[0]
     assert st == 0 and np.array_equal(r0, r1) and np.array_equal(c0, c1)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_sparse_cubes_batched_equal_scipy(cuda, dtype):
+    """The candidate-list kernels on real flattened cubes of 40-130
+    detections per view (ragged, several per launch), with duplicated
+    detections (exact ties across columns) in some, against scipy."""
+    from bpc_baseline_amd.synth import make_capture
+    from oracle import oracle as O
+    rng = np.random.default_rng(5)
+    flats = []
+    for k in range(10):
+        n = [int(x) for x in rng.integers(40, 131, 3)]
+        Ks, RTs, dets = make_capture(np.random.default_rng(100 + k), 3, n, duplicates=3 * (k % 3))
+        from bpc_baseline_amd.inference.utils.camera_utils import camera_pairs, fundamental_matrices
+        F = fundamental_matrices(Ks, RTs, camera_pairs(3))
+        pts = np.concatenate([np.array([d["bb_center"] for d in dets[c]]) for c in range(3)])
+        cnt = [len(dets[c]) for c in range(3)]
+        co = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+        cube = O.cube(pts, co, np.asarray(F).reshape(3, 9), 1)[0]
+        flats.append(cube.reshape(cnt[0] * cnt[1], cnt[2]).astype(dtype))
+    for f, (r, c, st) in zip(flats, _batched(cuda, flats, {"lsap_sparse_min_cols": 1025}, dtype=dtype)):
+        r0, c0 = scipy_lsa(f)
+        assert st == 0 and np.array_equal(r, r0) and np.array_equal(c, c0), f.shape
 
 
 @pytest.mark.parametrize("shapes", [
