@@ -560,14 +560,21 @@ def run_match(args, env, wl, kernel_options):
     offs = tplan.cube_offs[:-1].contiguous()
     threshold = float(wl["threshold"])
     stream = torch.cuda.current_stream(dev)
+    # the cube kernel also writes its 8-row minima, which the assignment
+    # reduces instead of reading the 67 GB of cubes once more (--lsap-input cost: off)
+    bm8 = (torch.empty(max(tplan.n_bmin8, 1), dtype=torch.int32, device=dev)
+           if args.lsap_input == "bmin8" else None)
+    bm8_args = (bm8, tplan.bmin8_offs, tplan.segs) if bm8 is not None else None
 
     def step(ev=None):
         if ev:
             ev[0].record(stream)
-        ops.triplet_cost_argmin(pts, cam_offs, F, tplan, out=(cube, am, mv), options=kernel_options)
+        ops.triplet_cost_argmin(pts, cam_offs, F, tplan, out=(cube, am, mv), options=kernel_options,
+                                bmin8=bm8)
         if ev:
             ev[1].record(stream)
-        r, c, st = ops.linear_sum_assignment_batched(cube, offs, lplan, options=kernel_options)
+        r, c, st = ops.linear_sum_assignment_batched(cube, offs, lplan, options=kernel_options,
+                                                     bmin8=bm8_args)
         if ev:
             ev[2].record(stream)
         res = ops.select_triangulate(cube, tplan.cube_offs, cam_offs, lplan.out_offs, r, c, pts,
@@ -626,9 +633,11 @@ def run_match(args, env, wl, kernel_options):
     value = total * args.steps / elapsed
     counts = batch.counts()
     cb = cube_bytes(counts)
-    # every cost entry must be read at least once by any exact assignment:
-    # that floor is the assignment stage's algorithmic traffic
-    lsap_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
+    # the assignment's streamed input: the cube's 8-row minima (default), or
+    # every cost entry once (--lsap-input cost: the floor for a solver that
+    # reads the cost itself)
+    cost_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
+    lsap_bytes = 4.0 * float(tplan.n_bmin8) if bm8 is not None else cost_bytes
     stages = {"cube": (cube_ms, cb, "triplet_fused_kernel"),
               "lsap": (lsap_ms, lsap_bytes, "mvm_lsap_solve kernels"),
               "select": (sel_ms, 0.0, "select_triangulate_kernel")}
@@ -659,13 +668,16 @@ def run_match(args, env, wl, kernel_options):
         "config": {"workload": wl["desc"], "n_cams": 3, "n_dets": wl["n_dets"],
                    "n_scenes_per_gpu": n_local, "n_scenes_total": total,
                    "matching_threshold": threshold, "kernel_options": kernel_options,
+                   "lsap_input": args.lsap_input,
                    "launch": "eager op calls (the assignment's launch is cooperative)",
                    "parallelism": f"scene-sharded x{world}" if env.initialised else "single GPU"},
         "stages_ms": {"cube": cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
                       "note": "rank 0, HIP events on the launch stream, mean over the timed steps"},
         "lsap": {"problems": n_local, "shape": f"{int(counts[0, 0] * counts[0, 1])} x {int(counts[0, 2])}",
                  "ms_per_batch": lsap_ms, "ms_per_problem": lsap_ms / max(1, n_local),
-                 "cost_gb_read_floor": lsap_bytes / 1e9},
+                 "streamed_gb": lsap_bytes / 1e9, "cost_gb": cost_bytes / 1e9,
+                 "input": ("the cube kernel's 8-row minima (mvm_lsap_solve_ex3)" if bm8 is not None
+                           else "the cost cubes (mvm_lsap_solve_ex2)")},
         "matches_per_step": n_matches,
         "sclk": clocks.summary("sclk"),
         "roofline": {"bound": "hbm", "stage": dom, "kernel": d_kernel, "achieved": achieved,
@@ -673,8 +685,8 @@ def run_match(args, env, wl, kernel_options):
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
                      "bytes_per_launch": d_bytes, "avg_launch_ms": d_ms,
                      "note": ("the slowest stage; its algorithmic bytes: the cube's writes (4 B "
-                              "per triple + 8 B per row + inputs), or for the assignment the cost "
-                              "cube read once (4 B per entry)")},
+                              "per triple + 8 B per row + inputs), or for the assignment its "
+                              "streamed input (lsap.streamed_gb)")},
         "cpu_baseline": cpu,
         "parity": f"{'equal' if parity_ok else 'MISMATCH'} vs the CPU chain on {len(detail)} scenes",
         "parity_detail": detail,
@@ -727,6 +739,9 @@ def main():
                     help="mvm_options fields for the launches (include/mvmatch.h; e.g. "
                          "pairwise_row_groups=2): kernel-path choices that never change results, "
                          "for A/B runs of the line itself; recorded in config.kernel_options")
+    ap.add_argument("--lsap-input", choices=["bmin8", "cost"], default="bmin8",
+                    help="c2match: the assignment's block minima from the cube kernel's 8-row "
+                         "minima (default) or from reading the cost cubes again")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group (gloo, host only) and print the "
                          "world each rank joined; no GPU work (tests the launcher on a CPU host)")

@@ -36,7 +36,8 @@ class MvmOptions(ctypes.Structure):
         "cube_kernel", "cube_rows_per_instr", "lsap_wave_max_cols", "lsap_multi_g",
         "lsap_lds_max_cols", "lsap_lds_small_cols", "lsap_mid_max_cols", "lsap_reg_max_cols",
         "lsap_reg_threads", "lsap_mreg_max_cols", "pairwise_row_interleave",
-        "cube_cols_per_lane", "pairwise_xcd_fronts", "lsap_sparse_min_cols")]
+        "cube_cols_per_lane", "pairwise_xcd_fronts", "lsap_sparse_min_cols",
+        "lsap_sparse_blocks")]
 
 
 OPTION_FIELDS = [n for n, _ in MvmOptions._fields_[1:]]
@@ -108,6 +109,11 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _i32,
         _vp, _vp, _vp, _vp, _vp,
         _vp, _sz, _vp, _vp]),               # workspace, bytes, options (host), stream
+    "mvm_triplet_cost_argmin_bmin8": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _i32,
+        _vp, _vp, _vp, _vp, _vp,
+        _vp, _vp,                           # bmin8, bmin8_offs
+        _vp, _sz, _vp, _vp]),               # workspace, bytes, options (host), stream
     "mvm_lsap_plan": (_i64, [_i32, _vp, _vp, _vp, _vp]),
     "mvm_lsap_plan_ex": (_i64, [_i32, _vp, _vp, _i32, _vp, _vp]),
     "mvm_lsap_solve": (ctypes.c_int, [
@@ -125,6 +131,11 @@ SIGNATURES = {
         _vp, _i32, _vp, _vp, _i32, _vp, _vp,
         _vp, _sz, _vp, _vp, _vp,
         _i64, _i64, _i64, _vp, _vp]),       # long_min, long_max, short_max, options, stream
+    "mvm_lsap_solve_ex3": (ctypes.c_int, [
+        _vp, _i32, _vp, _vp, _i32, _vp, _vp,
+        _vp, _sz, _vp, _vp, _vp,
+        _i64, _i64, _i64,
+        _vp, _vp, _vp, _vp, _vp]),          # bmin8, bmin8_offs, segs, options, stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
         ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id

@@ -384,7 +384,33 @@ struct CubeFusedArgs {
     int32_t *argmin;
     float *minval;
     int32_t j_blocks, i_blocks;
+    // optional (BM8 instantiations): per (scene, i, group of 8 j rows) the
+    // minimum over the group of every k, as order-preserving keys (NaN ->
+    // kBm8NaN): row (i * ceil(M/8) + j/8) of P keys at bmin8 + bmin8_offs[s].
+    // The candidate-list assignment (mvm_lsap_sparse.hip) reduces these
+    // instead of reading the cube once more.
+    uint32_t *bmin8;
+    const int64_t *bmin8_offs;
 };
+
+// order-preserving key of a cube value (>= +0, +inf or NaN) for bmin8
+constexpr uint32_t kBm8NaN = 0xFFFFFFFEu;
+__device__ __forceinline__ uint32_t bm8_key(float v) {
+    return v != v ? kBm8NaN : (__float_as_uint(v) | 0x80000000u);
+}
+
+// one lane's KPL keys of an 8-row group (k = kb .. kb + KPL - 1, kvalid of them in the view)
+template <int KPL>
+__device__ __forceinline__ void bm8_store(uint32_t *row, int kb, int kvalid, const uint32_t (&k)[KPL],
+                                          bool vec) {
+    if (KPL == 4 && vec && kvalid >= 4) {
+        *reinterpret_cast<uint4 *>(row + kb) = make_uint4(k[0], k[1], k[2], k[KPL - 1]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < KPL; ++q)
+            if (q < kvalid) row[kb + q] = k[q];
+    }
+}
 
 struct LineRec {
     double l0, l1, l2;
@@ -416,9 +442,12 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // KPL: k per lane.  3 where the view fits 3 * (64 / SPLIT) k (48 / 96 / 192):
 // a quarter fewer VALU per row step than 4 k per lane, whose last quarter of
 // lanes would hold no k there; rows are stored with `global_store_dwordx3`.
-template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane>
-__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2 : kCubeRPW > 8 ? 3 : 4)   // 48-j tiles: 43 KB of LDS, 3 per CU
+template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane, bool BM8 = false>
+// 48-j tiles: 43 KB of LDS, 3 per CU; the 8-row minima at 4 k per lane need
+// more than 128 VGPRs (48 spilled at 4 workgroups per CU): 3 per CU
+__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2 : (kCubeRPW > 8 || (BM8 && KPL == 4)) ? 3 : 4)
 void triplet_fused_kernel(CubeFusedArgs args) {
+    static_assert(!BM8 || (SPLIT == 1 && kCubeRPW == 8), "8-row minima: one row per instruction, 8 per wave");
     constexpr bool HALF = SPLIT > 1;   // split mapping
     static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)),
                   "8 or 12 rows in 2 or 4 groups");
@@ -615,6 +644,9 @@ void triplet_fused_kernel(CubeFusedArgs args) {
             }
             uint32_t key[kLaneRows];
             int32_t idx[kLaneRows];
+            uint32_t bmk[KPL];                                   // BM8: the 8 rows' minima per k
+#pragma unroll
+            for (int q = 0; q < KPL; ++q) bmk[q] = 0xFFFFFFFFu;
 #pragma unroll
             for (int r = 0; r < kLaneRows; ++r) {
                 key[r] = kKeyInvalid;
@@ -647,6 +679,11 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                                 if (q < kvalid) args.cube[coff + row * P + kb + q] = v[q];
                         }
                     }
+                    if constexpr (BM8) {
+#pragma unroll
+                        for (int q = 0; q < KPL; ++q)
+                            if (act && (whole || q < kvalid)) bmk[q] = umin(bmk[q], bm8_key(v[q]));
+                    }
                     Best b{v[0], kb};
 #pragma unroll
                     for (int q = 1; q < KPL; ++q)
@@ -671,11 +708,17 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                             if (args.cube)
                                 args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
                             best_update_safe(b, v[q], kb + q);
+                            if constexpr (BM8) bmk[q] = umin(bmk[q], bm8_key(v[q]));
                         }
                     }
                     key[r] = best_key(b);
                     idx[r] = b.j;
                 }
+            }
+            if constexpr (BM8) {
+                if (act_k)
+                    bm8_store<KPL>(args.bmin8 + args.bmin8_offs[s] + ((int64_t)i * ((M + 7) / 8) + j0 / 8) * P,
+                                   kb, kvalid, bmk, (P & 3) == 0);
             }
             if constexpr (HALF) {
                 // each row lies on one group of kLPR lanes: reduce inside the
@@ -756,6 +799,9 @@ void triplet_fused_kernel(CubeFusedArgs args) {
             }
             uint32_t key[kCubeRPW];
             int32_t idx[kCubeRPW];
+            uint32_t bmk[kColsPerLane];                          // BM8: the 8 rows' minima per k
+#pragma unroll
+            for (int q = 0; q < kColsPerLane; ++q) bmk[q] = 0xFFFFFFFFu;
             uint64_t p = rp;
 #pragma unroll
             for (int r = 0; r < kCubeRPW; ++r) {
@@ -772,11 +818,25 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 const uint32_t b0 = __float_as_uint(v[0]), b1 = __float_as_uint(v[1]);
                 const uint32_t b2 = __float_as_uint(v[2]), b3 = __float_as_uint(v[3]);
                 const uint32_t m = umin(min3_u32(b0, b1, b2), b3);
+                if constexpr (BM8) {                             // finite, >= +0: the bits order
+                    bmk[0] = umin(bmk[0], b0);
+                    bmk[1] = umin(bmk[1], b1);
+                    bmk[2] = umin(bmk[2], b2);
+                    bmk[3] = umin(bmk[3], b3);
+                }
                 int q = (b2 == m) ? 2 : 3;
                 q = (b1 == m) ? 1 : q;
                 q = (b0 == m) ? 0 : q;
                 key[r] = m;                       // the bits themselves: no NaN / invalid here
                 idx[r] = kb + q;
+            }
+            if constexpr (BM8) {
+                uint32_t kk[kColsPerLane];
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) kk[q] = bmk[q] | 0x80000000u;
+                bm8_store<kColsPerLane>(args.bmin8 + args.bmin8_offs[s] +
+                                            ((int64_t)(ib + i_stride * ii) * ((M + 7) / 8) + j0 / 8) * P,
+                                        kb, kColsPerLane, kk, true);
             }
             uint32_t mk;
             int32_t mi;
@@ -1257,6 +1317,34 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
     }
 }
 
+// CubeFusedArgs::bmin8 read back from a finished cube, for the kernel paths
+// that do not emit the 8-row minima themselves: one workgroup per (scene, i).
+__global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t *cam_offs,
+                                                                   const int64_t *cube_offs,
+                                                                   const float *cube, uint32_t *bmin8,
+                                                                   const int64_t *bmin8_offs, int max_n) {
+    const int s = (int)(blockIdx.x / (unsigned)max_n), i = (int)(blockIdx.x % (unsigned)max_n);
+    const int64_t *co = cam_offs + 3 * (int64_t)s;
+    const int N = (int)(co[1] - co[0]), M = (int)(co[2] - co[1]), P = (int)(co[3] - co[2]);
+    if (i >= N || M == 0 || P == 0) return;
+    const int g8 = (M + 7) / 8;
+    const float *base = cube + cube_offs[s] + (int64_t)i * M * P;
+    uint32_t *out = bmin8 + bmin8_offs[s] + (int64_t)i * g8 * P;
+    for (int jg = 0; jg < g8; ++jg) {
+        for (int k = threadIdx.x; k < P; k += kThreads) {
+            uint32_t m = 0xFFFFFFFFu;
+            for (int j = 8 * jg; j < min(8 * jg + 8, M); ++j) m = umin(m, bm8_key(base[(int64_t)j * P + k]));
+            out[(int64_t)jg * P + k] = m;
+        }
+    }
+}
+
+int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
+                int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
+                const int64_t *row_offs_dev, float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
+                size_t workspace_bytes, const mvm_options *opts, hipStream_t s, bool &emitted);
+
 int grid_check(int64_t blocks) {
     if (blocks > kMaxGridBlocks)
         return mvm_fail(MVM_ERR_UNSUPPORTED, "grid of %lld workgroups too large: split the scenes",
@@ -1292,13 +1380,50 @@ size_t mvm_triplet_workspace_bytes(int32_t n_scenes, int32_t max_n) {
     return (size_t)n_scenes * 3 * (size_t)max_n * (size_t)ld * sizeof(double);
 }
 
+int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs_dev,
+                                  const double *F_dev, int32_t n_scenes, int32_t max_n,
+                                  const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                                  float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                                  uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                                  void *workspace_dev, size_t workspace_bytes,
+                                  const mvm_options *opts, mvm_stream_t stream) {
+    mvm_clear_error();
+    if (bmin8_dev && (!bmin8_offs_dev || !cube_dev || !cube_offs_dev))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "bmin8 needs its offsets and the cube");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    bool emitted = false;
+    int st = cube_launch(pts_dev, cam_offs_dev, F_dev, n_scenes, max_n, cube_offs_dev, row_offs_dev,
+                         cube_dev, argmin_dev, minval_dev, bmin8_dev, bmin8_offs_dev, workspace_dev,
+                         workspace_bytes, opts, s, emitted);
+    if (st || !bmin8_dev || emitted || n_scenes == 0 || max_n == 0) return st;
+    const int64_t blocks = (int64_t)n_scenes * max_n;
+    if ((st = grid_check(blocks))) return st;
+    bmin8_from_cube_kernel<<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(
+        cam_offs_dev, cube_offs_dev, cube_dev, bmin8_dev, bmin8_offs_dev, max_n);
+    return mvm_check_launch("bmin8_from_cube_kernel");
+}
+
 int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_dev,
                                const double *F_dev, int32_t n_scenes, int32_t max_n,
                                const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                                float *cube_dev, int32_t *argmin_dev, float *minval_dev,
                                void *workspace_dev, size_t workspace_bytes,
                                const mvm_options *opts, mvm_stream_t stream) {
-    mvm_clear_error();
+    return mvm_triplet_cost_argmin_bmin8(pts_dev, cam_offs_dev, F_dev, n_scenes, max_n, cube_offs_dev,
+                                         row_offs_dev, cube_dev, argmin_dev, minval_dev, nullptr, nullptr,
+                                         workspace_dev, workspace_bytes, opts, stream);
+}
+
+}  // extern "C"
+
+namespace {
+
+// every cube path; `emitted`: the launched kernel wrote bmin8 itself
+int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
+                int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
+                const int64_t *row_offs_dev, float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
+                size_t workspace_bytes, const mvm_options *opts, hipStream_t s, bool &emitted) {
     mvm_options o;
     int st = mvm_resolve_options(opts, o);
     if (st) return st;
@@ -1321,7 +1446,6 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
         return mvm_fail(MVM_ERR_WORKSPACE, "workspace %zu bytes < required %zu", workspace_bytes, need);
     if (((uintptr_t)workspace_dev & 15) != 0)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "workspace not 16-byte aligned");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int kernel = o.cube_kernel;
 
     // the one-workgroup-per-scene kernel: by default up to kSmallAutoMaxN
@@ -1370,9 +1494,10 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty
         const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8;
-        const CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
-                                           cube_dev, argmin_dev, minval_dev, max_n, 16,
-                                           j48 ? 12 : 8);
+        CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
+                                     cube_dev, argmin_dev, minval_dev, max_n, 16, j48 ? 12 : 8);
+        c.bmin8 = bmin8_dev;
+        c.bmin8_offs = bmin8_offs_dev;
         const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
         if ((st = grid_check(blocks))) return st;
         const dim3 grid((unsigned)blocks), block(kThreads);
@@ -1388,6 +1513,10 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
         } else if (split == 2) {
             if (kpl == 3) triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
+        } else if (bmin8_dev) {                  // the 8-row minima from the same kernel
+            if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3, true><<<grid, block, 0, s>>>(c);
+            else triplet_fused_kernel<16, 8, 1, kColsPerLane, true><<<grid, block, 0, s>>>(c);
+            emitted = true;
         } else {
             if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8><<<grid, block, 0, s>>>(c);
@@ -1400,7 +1529,7 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
     const int64_t mat_stride = (int64_t)max_n * ld;
     const int32_t pa[3] = {0, 0, 1}, pb[3] = {1, 2, 2};
     st = mvm_pairwise_residual_f64(pts_dev, cam_offs_dev, F_dev, pa, pb, n_scenes, 3, 3, max_n,
-                                   mat_stride, ld, (double *)workspace_dev, stream);
+                                   mat_stride, ld, (double *)workspace_dev, reinterpret_cast<mvm_stream_t>(s));
     if (st) return st;
     if (kernel == MVM_CUBE_WORKSPACE && max_n <= kChunk) {
         Cube3Args c{};
@@ -1439,14 +1568,14 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
     return mvm_check_launch("triplet_kernel");
 }
 
-int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
-                            const double *F_dev, int32_t n_scenes, int32_t max_n,
-                            const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
-                            float *cube_dev, int32_t *argmin_dev, float *minval_dev,
-                            void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream) {
+}  // namespace
+
+extern "C" int mvm_triplet_cost_argmin(const double *pts_dev, const int64_t *cam_offs_dev,
+                                       const double *F_dev, int32_t n_scenes, int32_t max_n,
+                                       const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                                       float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                                       void *workspace_dev, size_t workspace_bytes, mvm_stream_t stream) {
     return mvm_triplet_cost_argmin_ex(pts_dev, cam_offs_dev, F_dev, n_scenes, max_n, cube_offs_dev,
                                       row_offs_dev, cube_dev, argmin_dev, minval_dev, workspace_dev,
                                       workspace_bytes, nullptr, stream);
 }
-
-}  // extern "C"

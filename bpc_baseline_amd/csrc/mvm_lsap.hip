@@ -66,6 +66,9 @@ struct LsapArgs {
     int32_t mreg_lo, mreg_max_cols, mreg_nr_cap;
     int32_t sparse_lo;          // > 0: long sides >= this (lsap_sparse_class) are solved by
                                 // the candidate-list kernels (mvm_lsap_sparse.hip)
+    const uint32_t *bmin8;      // optional inputs of those kernels (LsapSparseArgs)
+    const int64_t *bmin8_offs;
+    const int64_t *segs;
 };
 
 __device__ __forceinline__ bool in_sparse_class(const LsapArgs &a, int64_t R, int64_t K) {
@@ -75,8 +78,11 @@ __device__ __forceinline__ bool in_sparse_class(const LsapArgs &a, int64_t R, in
 // lsap_reg_kernel's class: short sides up to this (its row state is in LDS)
 constexpr int kRegMaxShort = 1024;
 constexpr int kRegMaxCols = 4096;      // 512 threads x 8 columns, or 1024 x 4
-// default lower bound of the candidate-list class (mvm_options.lsap_sparse_min_cols)
-constexpr int kSparseMinCols = 4097;
+// default lower bound of the candidate-list class (mvm_options.lsap_sparse_min_cols):
+// 1000 problems of 4096 x 64 take 1.29 ms with candidate lists against 1.66 with
+// the register-state workgroup; 3136 x 56 1.42 against 1.38, 2304 x 48 1.12
+// against 1.03 (tools/bench_lsap.py, profiles/r05/lsap_sparse/)
+constexpr int kSparseMinCols = 4096;
 
 __device__ __forceinline__ bool in_reg_class(const LsapArgs &a, int64_t R, int64_t K) {
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
@@ -1767,7 +1773,9 @@ int lsap_launch(LsapArgs a, int32_t n_problems, size_t sync_bytes, int64_t long_
             a.sparse_lo = sp_lo;
             LsapSparseArgs sa{a.cost, a.cost_offs, a.dims, a.ws_offs, a.ws, a.out_offs, a.row_ind,
                               a.col_ind, a.status, sp_lo, wave_max,
-                              (int32_t)(s_max < kSpMaxShort ? s_max : kSpMaxShort)};
+                              (int32_t)(s_max < kSpMaxShort ? s_max : kSpMaxShort),
+                              a.bmin8, a.bmin8_offs, a.segs,
+                              o.lsap_sparse_blocks ? o.lsap_sparse_blocks : kSpTB};
             const int st = sizeof(CT) == 8 ? lsap_sparse_launch_f64(sa, n_problems, long_max, s)
                                             : lsap_sparse_launch_f32(sa, n_problems, long_max, s);
             if (st != MVM_OK) return st;
@@ -2010,6 +2018,19 @@ int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *
                        int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                        int64_t long_min, int64_t long_max, int64_t short_max,
                        const mvm_options *opts, mvm_stream_t stream) {
+    return mvm_lsap_solve_ex3(cost_dev, cost_dtype, cost_offs_dev, dims_dev, n_problems, ws_offs_dev,
+                              out_offs_dev, workspace_dev, workspace_bytes, row_ind_dev, col_ind_dev,
+                              status_dev, long_min, long_max, short_max, nullptr, nullptr, nullptr,
+                              opts, stream);
+}
+
+int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *cost_offs_dev,
+                       const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                       const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                       int64_t long_min, int64_t long_max, int64_t short_max,
+                       const uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                       const int64_t *segs_dev, const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
     mvm_options o;
     int st = mvm_resolve_options(opts, o);
@@ -2018,6 +2039,9 @@ int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cost_dtype %d", (int)cost_dtype);
     if (o.lsap_multi_g > kMultiMaxG)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "lsap_multi_g %d > %d", (int)o.lsap_multi_g, kMultiMaxG);
+    if (o.lsap_sparse_blocks < 0 || o.lsap_sparse_blocks > 64)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "lsap_sparse_blocks %d not in 0..64",
+                        (int)o.lsap_sparse_blocks);
     if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
     if (n_problems == 0) return MVM_OK;
     // one workgroup of up to 1024 threads per problem: the dispatch packet's
@@ -2038,7 +2062,9 @@ int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *
                reinterpret_cast<unsigned char *>(
                    (reinterpret_cast<uintptr_t>(workspace_dev) + workspace_bytes - sync_bytes) &
                    ~(uintptr_t)255),   // at or after the per-problem regions (all 256-aligned)
-               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+               0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, bmin8_dev, bmin8_offs_dev, segs_dev};
+    if (bmin8_dev && (!bmin8_offs_dev || !segs_dev))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "bmin8 needs its offsets and segment lengths");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (cost_dtype == MVM_F64)
         return lsap_launch<double>(a, n_problems, sync_bytes, long_min, long_max, short_max, o, s);

@@ -10,7 +10,7 @@
 constexpr int kSpMaxCols = 65536;    // long sides up to this (16-bit column ids, 8 KB bitmaps)
 constexpr int kSpMaxShort = 1024;    // short sides up to this (4 slots per thread)
 constexpr int kSpBlock = 32;         // columns per block minimum
-constexpr int kSpTB = 16;            // candidate blocks per row: the list holds >= 16 entries
+constexpr int kSpTB = 16;            // default candidate blocks per row: the list holds >= 16 entries
 constexpr int kSpLCap = 128;         // entries per candidate list (more: the row is scanned densely)
 constexpr int kSpTileCols = 2048;    // columns per block-minimum workgroup
 
@@ -27,7 +27,26 @@ struct LsapSparseArgs {
     int32_t lo;                   // long sides >= lo (> wave_max, <= kSpMaxCols) with short
     int32_t wave_max;             // sides in [1, kSpMaxShort] are this class's
     int32_t s_cap;                // LDS sizing: every short side of the class is <= this
+    // optional: minima of 8 consecutive tall rows per short-side column, as
+    // written by mvm_triplet_cost_argmin_bmin8 (problem p's long side is
+    // segs[p]-row segments -- a cube's M -- each cut in groups of 8 rows:
+    // row g * ceil(seg/8) + j/8 of S keys at bmin8 + bmin8_offs[p])
+    const uint32_t *bmin8;
+    const int64_t *bmin8_offs;
+    const int64_t *segs;
+    int32_t tb;                   // candidate blocks per row (mvm_options.lsap_sparse_blocks)
 };
+
+constexpr int kSpMaxBlocks = 2048;   // block minima per row (32 keys per wave lane)
+
+// problem p's blocks come from bmin8: the segment length (a cube's M), else 0
+// (blocks of 32 over the whole long side, from the cost itself)
+__host__ __device__ inline int lsap_sparse_seg(const LsapSparseArgs &a, int p, bool tr, int L) {
+    if (!a.bmin8 || !a.bmin8_offs || !a.segs || !tr) return 0;
+    const int64_t seg = a.segs[p];
+    if (seg <= 0 || L % seg != 0) return 0;
+    return (L / seg) * ((seg + 31) / 32) <= kSpMaxBlocks ? (int)seg : 0;
+}
 
 __host__ __device__ inline bool lsap_sparse_class(int32_t lo, int32_t wave_max, int64_t R, int64_t K) {
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
@@ -47,8 +66,12 @@ __host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, siz
         o += (bytes + 255) & ~(size_t)255;
         return at;
     };
-    const int64_t nb = (L + kSpBlock - 1) / kSpBlock, nt = (L + kSpTileCols - 1) / kSpTileCols;
-    y.flags = take((size_t)nt * 4);                  // invalid-entry flag per column tile
+    // blocks per row: ceil(L/32) over the whole long side; with segments
+    // (lsap_sparse_seg) (L/seg) * ceil(seg/32) <= min(kSpMaxBlocks, L)
+    const int64_t nbf = (L + kSpBlock - 1) / kSpBlock, nbs = L < kSpMaxBlocks ? L : kSpMaxBlocks;
+    const int64_t nb = nbf > nbs ? nbf : nbs;
+    const int64_t nt = (L + kSpTileCols - 1) / kSpTileCols;
+    y.flags = take((size_t)(nt > 32 ? nt : 32) * 4);   // invalid-entry flag per tile
     y.bm = take((size_t)S * nb * elem);              // ordered keys of the block minima
     y.lcol = take((size_t)S * kSpLCap * 4);
     y.lval = take((size_t)S * kSpLCap * elem);

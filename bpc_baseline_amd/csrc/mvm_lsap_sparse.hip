@@ -17,7 +17,7 @@
 //                        of each 32-column block of each short-side row, as
 //                        ordered integer keys; NaN / -inf flag the problem;
 //   sp_lists_kernel      one wave per short-side row: theta = the 16th
-//                        smallest block minimum; the list = every column with
+//                        smallest of the lanes' block minima; the list = every column with
 //                        cost <= theta (>= 16 entries, <= 128, else the row
 //                        is scanned densely when it is needed);
 //   sp_solve_kernel      one 256-thread workgroup per problem: per step the
@@ -125,6 +125,21 @@ __device__ __forceinline__ int sp_mbcnt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
+// n / d and n % d for 0 <= n, d < 2^22 from a float reciprocal rd = 1/d: the
+// estimate is within one of the quotient, one correction step makes it exact
+__device__ __forceinline__ int sp_div(int n, int d, float rd, int &r) {
+    int q = (int)((float)n * rd);
+    r = n - q * d;
+    if (r < 0) {
+        --q;
+        r += d;
+    } else if (r >= d) {
+        ++q;
+        r -= d;
+    }
+    return q;
+}
+
 // ---- 1. block minima ---------------------------------------------------------
 
 // W[s][j] (short-side row s, long-side column j) of a problem
@@ -137,7 +152,7 @@ template <typename CT>
 __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, int32_t n, int32_t tpp) {
     using K = SpKey<CT>;
     using KT = typename K::T;
-    constexpr int kKeys = 65536 / (int)sizeof(KT);         // 64 KiB of LDS keys per pass
+    constexpr int kKeys = 32768 / (int)sizeof(KT);         // 32 KiB of LDS keys per pass
     constexpr int VW = 16 / (int)sizeof(CT);               // elements per 16-byte load
     __shared__ KT s_key[kKeys];
     const int p = (int)(blockIdx.x / (unsigned)tpp), w = (int)(blockIdx.x % (unsigned)tpp);
@@ -146,6 +161,7 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
     if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
     const bool tr = Kd < R;
     const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
+    if (lsap_sparse_seg(a, p, tr, L)) return;              // sp_bmin8_reduce_kernel's
     const int j0 = w * kSpTileCols;
     if (j0 >= L) return;
     const int j1 = min(j0 + kSpTileCols, L);
@@ -173,24 +189,36 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
 #pragma unroll
             for (int v = 0; v < VW; ++v) run[v] = K::kMax;
             int cur = r0 >> 5;
-            for (int r = r0; r < nr; r += q) {
-                const int blk = r >> 5;
-                if (blk != cur) {
+            // eight 16-byte loads in flight per thread, then their minima
+            for (int rb = r0; rb < nr; rb += 8 * q) {
+                uint4 raw[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = rb + u * q;
+                    raw[u] = r < nr ? *reinterpret_cast<const uint4 *>(C0 + (int64_t)(pj0 + r) * S + g * VW)
+                                    : make_uint4(0u, 0u, 0u, 0u);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int r = rb + u * q;
+                    if (r >= nr) continue;
+                    const int blk = r >> 5;
+                    if (blk != cur) {
+#pragma unroll
+                        for (int v = 0; v < VW; ++v) {
+                            atomicMin(&s_key[(g * VW + v) * bp + cur], run[v]);
+                            run[v] = K::kMax;
+                        }
+                        cur = blk;
+                    }
+                    CT val[VW];
+                    *reinterpret_cast<uint4 *>(val) = raw[u];
 #pragma unroll
                     for (int v = 0; v < VW; ++v) {
-                        atomicMin(&s_key[(g * VW + v) * bp + cur], run[v]);
-                        run[v] = K::kMax;
+                        bad |= sp_invalid(val[v]);
+                        const KT kk = K::of(val[v]);
+                        run[v] = kk < run[v] ? kk : run[v];
                     }
-                    cur = blk;
-                }
-                CT val[VW];
-                *reinterpret_cast<uint4 *>(val) =
-                    *reinterpret_cast<const uint4 *>(C0 + (int64_t)(pj0 + r) * S + g * VW);
-#pragma unroll
-                for (int v = 0; v < VW; ++v) {
-                    bad |= sp_invalid(val[v]);
-                    const KT kk = K::of(val[v]);
-                    run[v] = kk < run[v] ? kk : run[v];
                 }
             }
             if (r0 < nr) {
@@ -243,6 +271,111 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
     if (t == 0) reinterpret_cast<int32_t *>(ws + y.flags)[w] = bad;
 }
 
+// ---- 1'. block minima from a cube's 8-row minima ------------------------------
+// Problem p with lsap_sparse_seg(p) = seg (a cube's M): block (g, jt) is the
+// columns g*seg + [32 jt, min(32 jt + 32, seg)), i.e. the 8-row groups 4 jt ..
+// 4 jt + 3 of segment g, whose minima mvm_triplet_cost_argmin_bmin8 wrote:
+// a few MB per problem are read instead of the whole cost.  One workgroup per
+// 64 blocks; NaN / -inf keys flag the problem.
+__global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a, int32_t n) {
+    constexpr int kKeys = 8192;                            // 32 KiB of LDS keys per pass
+    constexpr int kTiles = kSpMaxBlocks / 64;
+    __shared__ uint32_t s_key[kKeys];
+    const int p = (int)(blockIdx.x / kTiles), w = (int)(blockIdx.x % kTiles);
+    if (p >= n) return;
+    const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
+    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
+    const bool tr = Kd < R;
+    const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
+    const int seg = lsap_sparse_seg(a, p, tr, L);
+    if (!seg) return;
+    const int bps = (seg + 31) / 32, bps8 = (seg + 7) / 8, nb = (L / seg) * bps;
+    const int b0 = w * 64;
+    if (b0 >= nb) return;
+    const int b1 = min(b0 + 64, nb);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(float));
+    unsigned char *ws = a.ws + a.ws_offs[p];
+    uint32_t *bm = reinterpret_cast<uint32_t *>(ws + y.bm);
+    const uint32_t *B8 = a.bmin8 + a.bmin8_offs[p];
+    int bp = 64;
+    while (bp > 1 && S * bp > kKeys) bp >>= 1;
+    const int t = threadIdx.x;
+    const int G = S / 4;
+    const bool fast = S % 4 == 0 && kSpNT % G == 0 && ((reinterpret_cast<uintptr_t>(B8)) & 15) == 0;
+    auto invalid = [](uint32_t k) { return k <= 0x007FFFFFu || k > 0xFF800000u; };   // -inf / NaN
+    int bad = 0;
+    for (int pb0 = b0; pb0 < b1; pb0 += bp) {
+        const int pb1 = min(pb0 + bp, b1), nrow = 4 * (pb1 - pb0);   // (block, u) rows
+        for (int x = t; x < S * bp; x += kSpNT) s_key[x] = 0xFFFFFFFFu;
+        __syncthreads();
+        // local row x -> its 8-row group, or -1 past the segment's end
+        auto group = [&](int x) {
+            const int b = pb0 + (x >> 2), u = x & 3;
+            const int g = b / bps, jt = b - g * bps;
+            return 4 * jt + u < bps8 ? g * bps8 + 4 * jt + u : -1;
+        };
+        if (fast) {
+            // thread: keys 4 g4 .. 4 g4 + 3 of blocks lb = t / G + q m, each
+            // block's (up to) four 8-row groups loaded together, two blocks at
+            // a time (eight 16-byte loads in flight); one thread per (key, block):
+            // plain LDS stores
+            const int q = kSpNT / G, g4 = t % G, nbk = pb1 - pb0;
+            for (int lb0 = t / G; lb0 < nbk; lb0 += 2 * q) {
+                uint4 v[2][4];
+                bool ok[2][4];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int lb = lb0 + h * q;
+                        const int r = lb < nbk ? group(4 * lb + u) : -1;
+                        ok[h][u] = r >= 0;
+                        v[h][u] = ok[h][u] ? *reinterpret_cast<const uint4 *>(B8 + (int64_t)r * S + 4 * g4)
+                                           : make_uint4(~0u, ~0u, ~0u, ~0u);
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int lb = lb0 + h * q;
+                    if (lb >= nbk) continue;
+                    uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (!ok[h][u]) continue;
+                        const uint4 x = v[h][u];
+                        bad |= invalid(x.x) | invalid(x.y) | invalid(x.z) | invalid(x.w);
+                        m.x = min(m.x, x.x);
+                        m.y = min(m.y, x.y);
+                        m.z = min(m.z, x.z);
+                        m.w = min(m.w, x.w);
+                    }
+                    s_key[(4 * g4 + 0) * bp + lb] = m.x;
+                    s_key[(4 * g4 + 1) * bp + lb] = m.y;
+                    s_key[(4 * g4 + 2) * bp + lb] = m.z;
+                    s_key[(4 * g4 + 3) * bp + lb] = m.w;
+                }
+            }
+        } else {
+            for (int e = t; e < nrow * S; e += kSpNT) {
+                const int x = e / S, sc = e - x * S, r = group(x);
+                if (r < 0) continue;
+                const uint32_t v = B8[(int64_t)r * S + sc];
+                bad |= invalid(v);
+                atomicMin(&s_key[sc * bp + (x >> 2)], v);
+            }
+        }
+        __syncthreads();
+        const int nbk = pb1 - pb0;
+        for (int x = t; x < S * nbk; x += kSpNT) {
+            const int sc = x / nbk, bb = x - sc * nbk;
+            bm[(int64_t)sc * nb + pb0 + bb] = s_key[sc * bp + bb];
+        }
+        __syncthreads();
+    }
+    bad = __syncthreads_or(bad);
+    if (t == 0) reinterpret_cast<int32_t *>(ws + y.flags)[w] = bad;
+}
+
 // ---- 2. candidate lists --------------------------------------------------------
 
 template <typename CT>
@@ -265,7 +398,11 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     int32_t *ln = reinterpret_cast<int32_t *>(ws + y.ln);
     CT *theta_out = reinterpret_cast<CT *>(ws + y.theta);
     const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
-    const int nb = (L + kSpBlock - 1) / kSpBlock;
+    // blocks: 32 columns over the whole long side, or (a cube's) segments of
+    // seg columns cut in blocks of 32 (block b = segment b / bps, part b % bps)
+    const int seg0 = lsap_sparse_seg(a, p, tr, L), seg = seg0 ? seg0 : L;
+    const int bps = (seg + kSpBlock - 1) / kSpBlock, nb = (L / seg) * bps;
+    const float rbps = 1.0f / (float)bps;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int s = grp * (kSpNT / 64) + wave; s < S; s += kSpRowGroups * (kSpNT / 64)) {
         KT k[kQ];
@@ -276,14 +413,18 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         }
         KT thr = K::kMax;
         CT theta = (CT)INFINITY;
-        if (nb > kSpTB) {                                  // the kSpTB-th smallest key
+        if (nb > a.tb) {
+            // theta: the tb-th smallest of the 64 lanes' minima (lane l holds
+            // blocks l, l + 64, ...), so >= tb blocks hold a cost <= theta;
+            // a search over one value per lane (32 steps of one compare), where
+            // the tb-th smallest block minimum itself took 32 compares per step
+            KT lm = k[0];
+#pragma unroll
+            for (int q = 1; q < kQ; ++q) lm = k[q] < lm ? k[q] : lm;
             KT lo = 0, hi = K::kMax;
             while (lo < hi) {
                 const KT mid = lo + (hi - lo) / 2;
-                int cnt = 0;
-#pragma unroll
-                for (int q = 0; q < kQ; ++q) cnt += __popcll(__ballot(k[q] <= mid));
-                if (cnt >= kSpTB) hi = mid;
+                if (__popcll(__ballot(lm <= mid)) >= a.tb) hi = mid;
                 else lo = mid + 1;
             }
             thr = lo;
@@ -296,7 +437,12 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             const uint64_t m = __ballot(c);
             if (c) {
                 const int pos = ncand + sp_mbcnt(m);
-                if (pos < kSpLCap) s_cand[wave][pos] = lane + 64 * q;
+                if (pos < kSpLCap) {                        // the block's first column | its width << 16
+                    int jt;
+                    const int g = sp_div(lane + 64 * q, bps, rbps, jt);
+                    const int j0 = g * seg + jt * kSpBlock;
+                    s_cand[wave][pos] = j0 | (min(kSpBlock, seg - jt * kSpBlock) << 16);
+                }
             }
             ncand += __popcll(m);
         }
@@ -310,9 +456,9 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int idx = m0 + 2 * u + (lane >> 5);
-                    const int blk = idx < ncand ? s_cand[wave][idx] : -1;
-                    const int j = blk * kSpBlock + (lane & 31);
-                    col[u] = (blk >= 0 && j < L) ? j : -1;
+                    const int cb = idx < ncand ? s_cand[wave][idx] : 0;
+                    const int j = (cb & 0xFFFF) + (lane & 31);
+                    col[u] = (lane & 31) < (cb >> 16) ? j : -1;
                     val[u] = col[u] >= 0 ? sp_w(C0, tr, S, L, s, j) : (CT)0;
                 }
 #pragma unroll
@@ -420,7 +566,9 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
 
     // NaN / -inf anywhere (sp_blockmin_kernel's tile flags): scipy's ValueError
     {
-        const int nt = (L + kSpTileCols - 1) / kSpTileCols;
+        const int seg = lsap_sparse_seg(a, p, tr, L);      // whose tiles wrote the flags
+        const int nt = seg ? ((L / seg) * ((seg + kSpBlock - 1) / kSpBlock) + 63) / 64
+                           : (L + kSpTileCols - 1) / kSpTileCols;
         const int32_t *fl = reinterpret_cast<const int32_t *>(ws + y.flags);
         int bad = 0;
         for (int x = t; x < nt; x += kSpNT) bad |= fl[x];
@@ -731,9 +879,17 @@ int sp_launch(const LsapSparseArgs &a0, int32_t n, int64_t long_max, hipStream_t
     LsapSparseArgs a = a0;
     const int64_t lmax = long_max < kSpMaxCols ? long_max : kSpMaxCols;
     const int tpp = (int)((lmax + kSpTileCols - 1) / kSpTileCols);
-    if ((int64_t)n * tpp * kSpNT > 0xFFFFFFFFLL || (int64_t)n * kSpRowGroups * kSpNT > 0xFFFFFFFFLL)
+    if ((int64_t)n * tpp * kSpNT > 0xFFFFFFFFLL || (int64_t)n * kSpRowGroups * kSpNT > 0xFFFFFFFFLL ||
+        (int64_t)n * (kSpMaxBlocks / 64) * kSpNT > 0xFFFFFFFFLL)
         return mvm_fail(MVM_ERR_UNSUPPORTED, "%d problems in one batch: split it", (int)n);
+    if (sizeof(CT) != sizeof(float)) {                      // the cube's minima are float keys
+        a.bmin8 = nullptr;
+        a.bmin8_offs = nullptr;
+        a.segs = nullptr;
+    }
     sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
+    if (a.bmin8)
+        sp_bmin8_reduce_kernel<<<dim3((unsigned)(n * (kSpMaxBlocks / 64))), dim3(kSpNT), 0, s>>>(a, n);
     sp_lists_kernel<CT><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
     const int cap = a.s_cap;
     const int lw = (int)(((lmax + 63) / 64) * 2);            // even: the f64 arrays stay 8-aligned

@@ -176,12 +176,7 @@ __device__ __forceinline__ void row_fast_lazy(const ColRegs &c, double rl0, doub
                                               double rx, double ry, float *drow, int jbase,
                                               uint32_t &bbits, bool st = true) {
     float v[kColsPerLane];
-#ifdef MVM_DIAG_NO_ARITH   // diagnostic build only (phase timing): the stores without the pair arithmetic
-#pragma unroll
-    for (int q = 0; q < kColsPerLane; ++q) v[q] = (float)(rx + c.x[q]);
-#else
     pair_bits4(c, rl0, rl1, rl2, rx, ry, v);
-#endif
     if (STORE && (!MASKED || st)) store4_nt_row<NT>(reinterpret_cast<uint64_t>(drow), (uint32_t)jbase * 4u, v);
     bbits = min3_u32(min3_u32(__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2])),
                      __float_as_uint(v[3]), bbits);
@@ -330,14 +325,7 @@ __device__ __forceinline__ void load_col_lines(const double *pts, const double (
         if (j < nb) {
             x = pts[2 * (ob + j)];
             y = pts[2 * (ob + j) + 1];
-#ifdef MVM_DIAG_CHEAP_LINES   // diagnostic build only (phase timing): unnormalised lines
-            l0 = f[0] * x;
-            l1 = f[4] * y;
-            l2 = f[8];
-            st = kOk;
-#else
             st = col_line(f, x, y, l0, l1, l2) ? kDeg : (tame(l2, x, y) ? kOk : kWild);
-#endif
         }
         s_l0[jj] = l0;
         s_l1[jj] = l1;
@@ -368,14 +356,7 @@ __device__ __forceinline__ void put_row_line(double *slot, const double *s_rpt,
     if (valid) {
         x = s_rpt[2 * lrow];
         y = s_rpt[2 * lrow + 1];
-#ifdef MVM_DIAG_CHEAP_LINES   // diagnostic build only (phase timing): unnormalised lines
-        l0 = f[0] * x;
-        l1 = f[4] * y;
-        l2 = f[8];
-        deg = false;
-#else
         deg = row_line(f, x, y, l0, l1, l2);
-#endif
     }
     slot[0] = l0;
     slot[1] = l1;
@@ -474,11 +455,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 ColRegs c;
 #pragma unroll
                 for (int q = 0; q < kColsPerLane; ++q) {
-#ifdef MVM_DIAG_OCC3_C3   // diagnostic build only (timing): a 640-column LDS tile reused
-                    const int jj = (jbase + q) % args.col_tile;
-#else
                     const int jj = jbase + q;
-#endif
                     c.l0[q] = s_l0[jj];
                     c.l1[q] = s_l1[jj];
                     c.l2[q] = s_l2[jj];
@@ -546,15 +523,6 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
             // reload drained all of them
             int lz = lane;
             __asm__ volatile("" : "+v"(lz));
-#ifdef MVM_DIAG_NO_ASSOC   // diagnostic build only (phase timing): no group reduction
-            {
-                uint32_t x = 0;
-#pragma unroll
-                for (int r = 0; r < RPW; ++r) x ^= bbits[r];
-                if (lz < RPW && args.minval) args.minval[g.row_off0 + grow0 + lz * RST] = __uint_as_float(x);
-                continue;
-            }
-#endif
             uint32_t k;
             int w;
             bool tie;
@@ -571,11 +539,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 const int c = idx / kColsPerLane, q = idx % kColsPerLane;
                 if (c < n_ch) {
                     const uint32_t b = pair_bits1(s_l0, s_l1, s_l2, s_x, s_y,
-#ifdef MVM_DIAG_OCC3_C3
-                                                  (c * kChunk + kColsPerLane * w + q) % args.col_tile, rl);
-#else
                                                   c * kChunk + kColsPerLane * w + q, rl);
-#endif
                     first = (b == k) ? (uint32_t)idx : first;
                 }
             }
@@ -589,11 +553,7 @@ __global__ __launch_bounds__(kThreads, OCC) void pairwise_lazy_kernel(PairArgs a
                 if (tie) {
                     uint32_t jt = 0xFFFFFFFFu;
                     for (int jj = nb - LPR + seg; jj >= 0; jj -= LPR)
-#ifdef MVM_DIAG_OCC3_C3
-                        jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj % args.col_tile, rl) == k)
-#else
                         jt = (pair_bits1(s_l0, s_l1, s_l2, s_x, s_y, jj, rl) == k)
-#endif
                                  ? (uint32_t)jj : jt;
                     jwin = (int)group_min_u32<RPW>(jt);
                 }
@@ -870,9 +830,6 @@ template <int RPW>
 int launch_pairwise_rpw(PairArgs &a, int64_t sp_count, int max_rows, int max_cols,
                         int row_groups, bool argmin, bool f64, hipStream_t stream) {
     a.col_tile = min(kMaxColTile, max(kChunk, (max_cols + kChunk - 1) / kChunk * kChunk));
-#ifdef MVM_DIAG_OCC3_C3   // diagnostic build only: LDS small enough for three workgroups per CU
-    if (max_cols > 2 * kChunk && row_groups <= 2) a.col_tile = 640;
-#endif
     a.rows_per_wg = kWaves * RPW * row_groups;
     a.row_blocks = (max_rows + a.rows_per_wg - 1) / a.rows_per_wg;
     const dim3 grid((unsigned)(sp_count * a.row_blocks)), block(kThreads);

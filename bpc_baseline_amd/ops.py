@@ -180,6 +180,65 @@ def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minv
     return None
 
 
+@torch.library.custom_op("mvmatch::triplet_cost_bmin8_out",
+                         mutates_args=("cube", "argmin", "minval", "bmin8", "workspace"))
+def triplet_cost_bmin8_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, max_n: int,
+                           cube_offs: Tensor, row_offs: Tensor, cube: Tensor, argmin: Tensor,
+                           minval: Tensor, bmin8: Tensor, bmin8_offs: Tensor, workspace: Tensor,
+                           opts: Optional[List[int]] = None) -> None:
+    """triplet_cost_argmin_out + the 8-row minima the assignment reduces
+    (mvm_triplet_cost_argmin_bmin8)."""
+    _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
+    for t, n, dt in ((cube_offs, "cube_offs", torch.int64), (row_offs, "row_offs", torch.int64),
+                     (cube, "cube", torch.float32), (argmin, "argmin", torch.int32),
+                     (minval, "minval", torch.float32), (bmin8, "bmin8", torch.int32),
+                     (bmin8_offs, "bmin8_offs", torch.int64), (workspace, "workspace", torch.uint8)):
+        _require(t, n, dt, pts.device)
+    st = _native.load().mvm_triplet_cost_argmin_bmin8(
+        _p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(cube_offs), _p(row_offs), _p(cube),
+        _p(argmin), _p(minval), _p(bmin8), _p(bmin8_offs), _p(workspace), workspace.numel(),
+        _opts_ref(opts), _stream(pts))
+    _native.check("mvm_triplet_cost_argmin_bmin8", st)
+
+
+@triplet_cost_bmin8_out.register_fake
+def _(pts, cam_offs, F, n_scenes, max_n, cube_offs, row_offs, cube, argmin, minval, bmin8, bmin8_offs,
+      workspace, opts=None):
+    return None
+
+
+@torch.library.custom_op("mvmatch::lsap_solve_bmin8_out",
+                         mutates_args=("workspace", "row_ind", "col_ind", "status"))
+def lsap_solve_bmin8_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
+                         out_offs: Tensor, workspace: Tensor, row_ind: Tensor, col_ind: Tensor,
+                         status: Tensor, bmin8: Tensor, bmin8_offs: Tensor, segs: Tensor,
+                         long_min: int, long_max: int, short_max: int,
+                         opts: Optional[List[int]] = None) -> None:
+    """lsap_solve_out taking a cube's 8-row minima (mvm_lsap_solve_ex3)."""
+    dev = cost.device
+    if dev.type != "cuda" or cost.dtype != torch.float32:
+        raise ValueError("cost must be a float32 GPU tensor")
+    for t, n, dt in ((cost_offs, "cost_offs", torch.int64), (dims, "dims", torch.int64),
+                     (ws_offs, "ws_offs", torch.int64), (out_offs, "out_offs", torch.int64),
+                     (workspace, "workspace", torch.uint8), (row_ind, "row_ind", torch.int64),
+                     (col_ind, "col_ind", torch.int64), (status, "status", torch.int32),
+                     (bmin8, "bmin8", torch.int32), (bmin8_offs, "bmin8_offs", torch.int64),
+                     (segs, "segs", torch.int64)):
+        _require(t, n, dt, dev)
+    st = _native.load().mvm_lsap_solve_ex3(_p(cost), _native.MVM_F32, _p(cost_offs), _p(dims),
+                                           status.numel(), _p(ws_offs), _p(out_offs), _p(workspace),
+                                           workspace.numel(), _p(row_ind), _p(col_ind), _p(status),
+                                           long_min, long_max, short_max, _p(bmin8), _p(bmin8_offs),
+                                           _p(segs), _opts_ref(opts), _stream(cost))
+    _native.check("mvm_lsap_solve_ex3", st)
+
+
+@lsap_solve_bmin8_out.register_fake
+def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, bmin8, bmin8_offs,
+      segs, long_min, long_max, short_max, opts=None):
+    return None
+
+
 @torch.library.custom_op("mvmatch::lsap_solve_out",
                          mutates_args=("workspace", "row_ind", "col_ind", "status"))
 def lsap_solve_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs: Tensor,
@@ -442,6 +501,13 @@ class TripletPlan:
         self.cube_offs, self.row_offs = _h2d_int64([cube_offs, row_offs], self.device)
         self.workspace_bytes = int(_native.load().mvm_triplet_workspace_bytes(self.n_scenes,
                                                                                self.max_n))
+        # the cube's 8-row minima for the assignment (mvm_triplet_cost_argmin_bmin8):
+        # N * ceil(M/8) rows of P keys per scene
+        bm8 = np.zeros(n_scenes + 1, np.int64)
+        np.cumsum(counts[:, 0] * ((counts[:, 1] + 7) // 8) * counts[:, 2], out=bm8[1:])
+        self.bmin8_offs_host = bm8
+        self.n_bmin8 = int(bm8[-1])
+        self.bmin8_offs, self.segs = _h2d_int64([bm8, np.ascontiguousarray(counts[:, 1])], self.device)
         self.workspace = torch.empty(max(self.workspace_bytes, 16), dtype=torch.uint8,
                                      device=self.device)
 
@@ -449,9 +515,11 @@ class TripletPlan:
 def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
                         want_cube: bool = True,
                         out: Optional[Tuple[Tensor, Tensor, Tensor]] = None,
-                        options: Optional[dict] = None):
+                        options: Optional[dict] = None, bmin8: Optional[Tensor] = None):
     """-> (cube f32 [plan.n_cube], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
-    ``options``: mvm_options fields, e.g. ``{"cube_kernel": "workspace"}``."""
+    ``options``: mvm_options fields, e.g. ``{"cube_kernel": "workspace"}``.
+    ``bmin8`` (int32 [plan.n_bmin8]): also the 8-row minima that
+    ``linear_sum_assignment_batched(..., bmin8=)`` reduces (needs the cube)."""
     dev = pts.device
     if out is None:
         cube = torch.empty(plan.n_cube if want_cube else 0, dtype=torch.float32, device=dev)
@@ -459,6 +527,11 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
         minval = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
     else:
         cube, argmin, minval = out
+    if bmin8 is not None:
+        torch.ops.mvmatch.triplet_cost_bmin8_out(
+            pts, cam_offs, F, plan.n_scenes, plan.max_n, plan.cube_offs, plan.row_offs, cube, argmin,
+            minval, bmin8, plan.bmin8_offs, plan.workspace, _opts_list(options))
+        return cube, argmin, minval
     torch.ops.mvmatch.triplet_cost_argmin_out(
         pts, cam_offs, F, plan.n_scenes, plan.max_n, plan.cube_offs, plan.row_offs, cube, argmin,
         minval, plan.workspace, _opts_list(options))
@@ -510,16 +583,26 @@ class LsapPlan:
 
 
 def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPlan, *,
-                                  options: Optional[dict] = None):
+                                  options: Optional[dict] = None,
+                                  bmin8: Optional[Tuple[Tensor, Tensor, Tensor]] = None):
     """scipy.optimize.linear_sum_assignment for every problem of ``plan`` on the GPU.
     -> (row_ind i64 [n_out], col_ind i64 [n_out], status i32 [n]) device tensors.
-    ``cost`` must have the plan's dtype."""
+    ``cost`` must have the plan's dtype.  ``bmin8`` = (keys, the TripletPlan's
+    bmin8_offs, its segs) when the costs are the flattened cubes of a
+    ``triplet_cost_argmin(..., bmin8=keys)`` call: the assignment then reduces
+    those instead of reading every cost once more (same result)."""
     if cost.dtype != plan.dtype:
         raise ValueError(f"cost is {cost.dtype} but the plan was built for {plan.dtype}")
     dev = cost.device
     row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)
+    if bmin8 is not None and cost.dtype == torch.float32:
+        torch.ops.mvmatch.lsap_solve_bmin8_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
+                                               plan.workspace, row_ind, col_ind, status, bmin8[0],
+                                               bmin8[1], bmin8[2], plan.long_min, plan.long_max,
+                                               plan.short_max, _opts_list(options))
+        return row_ind[:plan.n_out], col_ind[:plan.n_out], status
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
                                      plan.workspace, row_ind, col_ind, status, plan.long_min,
                                      plan.long_max, _opts_list(options), plan.short_max)

@@ -131,10 +131,12 @@ typedef struct mvm_options {
                                        matrices, else 1); 1..16: each XCD writes its
                                        eighth of the grid as this many concurrent
                                        contiguous ranges (ABI 5) */
-    int32_t lsap_sparse_min_cols;   /* 0 default (4097); -1 off: problems with a long
+    int32_t lsap_sparse_min_cols;   /* 0 default (4096); -1 off: problems with a long
                                        side >= this (and > the one-wave limit, <= 65536)
                                        and a short side <= 1024 are solved one workgroup
                                        each through per-row candidate lists (ABI 6) */
+    int32_t lsap_sparse_blocks;     /* 0 default (16): candidate blocks (of 32 columns)
+                                       per row of that class, 1..64 (ABI 6) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */
@@ -229,6 +231,22 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
                                float *cube_dev, int32_t *argmin_dev, float *minval_dev,
                                void *workspace_dev, size_t workspace_bytes,
                                const mvm_options *opts, mvm_stream_t stream);
+/*
+ * ... also writing, for the assignment that follows (mvm_lsap_solve_ex3), the
+ * minimum over every group of 8 consecutive j of every (i, k) (ABI 6): for
+ * scene s with view sizes N, M, P, row i * ceil(M/8) + g of P uint32 keys at
+ * bmin8_dev + bmin8_offs_dev[s] holds, per k, the order-preserving key
+ * (float bits | 0x80000000; NaN 0xFFFFFFFE) of min over j in [8g, 8g+8) of
+ * cube[i][j][k].  The fused kernel of views of 129-256 detections writes them
+ * itself; every other path reads them back from the cube (cube_dev required).
+ */
+int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs_dev,
+                                  const double *F_dev, int32_t n_scenes, int32_t max_n,
+                                  const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
+                                  float *cube_dev, int32_t *argmin_dev, float *minval_dev,
+                                  uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                                  void *workspace_dev, size_t workspace_bytes,
+                                  const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * Batched rectangular linear-sum assignment, identical to
@@ -287,6 +305,21 @@ int mvm_lsap_solve_ex2(const void *cost_dev, int32_t cost_dtype, const int64_t *
                        int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                        int64_t long_min, int64_t long_max, int64_t short_max,
                        const mvm_options *opts, mvm_stream_t stream);
+/*
+ * ... taking the block minima of cubes from mvm_triplet_cost_argmin_bmin8
+ * (ABI 6): problem p's cost is a flattened (N*M, P) cube (segs_dev[p] = M)
+ * whose 8-row minima are at bmin8_dev + bmin8_offs_dev[p].  The candidate-list
+ * kernels then read those (N * ceil(M/8) * P keys) instead of the whole cost
+ * once more; results are the same.  Ignored for float64 costs and for
+ * problems outside the class; all three pointers NULL = mvm_lsap_solve_ex2.
+ */
+int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *cost_offs_dev,
+                       const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                       const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                       int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                       int64_t long_min, int64_t long_max, int64_t short_max,
+                       const uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                       const int64_t *segs_dev, const mvm_options *opts, mvm_stream_t stream);
 
 /*
  * On-device detection packing, replacing the per-box loop of

@@ -22,8 +22,9 @@ sink), it is never removed from the scan before the search ends, and its
 * the at most S assigned columns are scanned explicitly ("slots").
 
 Each row keeps a candidate list: every column with ``C <= theta_s``, where
-``theta_s`` is the TB-th smallest of the row's block minima (blocks of B
-columns), so the list holds at least TB entries and every column outside it
+``theta_s`` is the TB-th smallest of the minima of 64 groups of the row's
+block minima (blocks of B columns, group l = blocks l, l+64, ...: one wave
+lane each), so the list holds at least TB entries and every column outside it
 has ``C >= beta_s = nextafter(theta_s, inf)``.  Its smallest free entry is the
 row's free minimum whenever the list holds a free entry; the list holds every
 free tie at ``lowest`` whenever ``r(beta_s) > lowest``.  Otherwise (or when
@@ -62,7 +63,12 @@ def candidate_lists(W: np.ndarray, B: int, TB: int, LCAP: int):
     bm = pad.reshape(S, nb, B).min(axis=2)
     out = []
     for s in range(S):
-        theta = np.sort(bm[s])[TB - 1] if nb > TB else W.dtype.type(np.inf)
+        # the kernel's rule: lane l of a wave holds blocks l, l + 64, ...;
+        # theta is the TB-th smallest of the 64 lanes' minima
+        lanes = np.full(64, np.inf, W.dtype)
+        for l in range(min(64, nb)):
+            lanes[l] = bm[s, l::64].min()
+        theta = np.sort(lanes)[TB - 1] if nb > TB else W.dtype.type(np.inf)
         cand = np.nonzero(bm[s] <= theta)[0]
         cols = (cand[:, None] * B + np.arange(B)[None, :]).reshape(-1)
         cols = cols[cols < L]

@@ -25,7 +25,7 @@ def _batched(cuda, mats, options=None, dtype=np.float32):
 
 
 @pytest.fixture(params=["default", "reg", "reg1024", "mreg", "lds", "workgroup", "workgroup256", "multi",
-                        "nomreg", "sparse", "sparse_lo"])
+                        "nomreg", "sparse", "sparse_lo", "sparse_tb1", "sparse_tb64"])
 def lsap_path(request):
     """mvm_options of each assignment kernel class.  default: long sides <=
     1024 one problem per wave, up to 4096 (short sides <= 1024) one workgroup
@@ -43,7 +43,9 @@ def lsap_path(request):
     side <= 1024 and a long side <= 65536 through the candidate-list kernels
     (the default above 4096 columns: mvm_lsap_sparse.hip), small ones (whose
     rows are all scanned densely) included; sparse_lo: the same from long
-    sides of 1025 on (lists and dense rows side by side).  Every other path
+    sides of 1025 on (lists and dense rows side by side); sparse_tb1 /
+    sparse_tb64: one / 64 candidate blocks per row (short lists that run out,
+    so rows fall back to dense scans, and long ones).  Every other path
     turns the candidate-list class off."""
     off = {"lsap_wave_max_cols": -1, "lsap_multi_g": -1, "lsap_mreg_max_cols": -1,
            "lsap_sparse_min_cols": -1}
@@ -58,7 +60,9 @@ def lsap_path(request):
                       "lsap_sparse_min_cols": -1},
             "nomreg": {"lsap_mreg_max_cols": -1, "lsap_sparse_min_cols": -1},
             "sparse": {"lsap_wave_max_cols": -1, "lsap_sparse_min_cols": 1},
-            "sparse_lo": {"lsap_sparse_min_cols": 1025}}[request.param]
+            "sparse_lo": {"lsap_sparse_min_cols": 1025},
+            "sparse_tb1": {"lsap_wave_max_cols": -1, "lsap_sparse_min_cols": 1, "lsap_sparse_blocks": 1},
+            "sparse_tb64": {"lsap_sparse_min_cols": 1025, "lsap_sparse_blocks": 64}}[request.param]
 
 
 def test_random_shapes_and_ties_batched(cuda, lsap_path):

@@ -33,7 +33,7 @@ ap.add_argument("--buffers", type=int, default=6)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--no-check", action="store_true",
                 help="skip the bit-equality check across builds (diagnostic builds, e.g. "
-                     "MVM_DIAG_CHEAP_LINES / MVM_DIAG_NO_ASSOC, compute other values)")
+                     "tools/diag cheap_lines / no_assoc patches, compute other values)")
 ap.add_argument("--scenes", type=int, default=None, help="scenes per launch (cube 250, c3 1000)")
 ap.add_argument("--dets", type=int, default=256, help="detections per view (cube)")
 ap.add_argument("--alloc", default=None,

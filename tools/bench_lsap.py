@@ -38,6 +38,14 @@ host0 = cube[: n * n * n].cpu().numpy().reshape(n * n, n)
 ts = time.perf_counter(); r0, c0 = scipy_lsa(host0); ts = time.perf_counter() - ts
 assert np.array_equal(r0, r1) and np.array_equal(c0, c1)
 tb, rb, cb = gpu_run(b.n_scenes)
+# the batch through each class, interleaved: candidate lists (the default for
+# long sides > 4096) vs the split register-state kernel (round 3/4 default)
+for rnd in range(3):
+    for name, opt in (("default", None), ("candidate lists from 1025", {"lsap_sparse_min_cols": 1025}),
+                      ("no candidate lists", {"lsap_sparse_min_cols": -1})):
+        tt, rr, cc = gpu_run(b.n_scenes, opt)
+        assert np.array_equal(rr, rb) and np.array_equal(cc, cb)
+        print(f"round {rnd} {name}: {b.n_scenes} x {n}^3 in {tt * 1e3:.2f} ms", flush=True)
 # spot-check the last scene of the batch
 last = cube[tp.cube_offs_host[-2]:tp.cube_offs_host[-1]].cpu().numpy().reshape(n * n, n)
 rl, cl = scipy_lsa(last)

@@ -8,6 +8,14 @@
 #   bash tools/gpu.sh pmc W [bench args]      FETCH_SIZE and WRITE_SIZE, one pass each
 #   bash tools/gpu.sh sq "PMC LIST" TOOL [args]  one --pmc pass over a tools/ script
 #   bash tools/gpu.sh py TOOL [args]          a tools/ script (or bench.py) under a time limit
+#   bash tools/gpu.sh final [W ...]           check, then per workload (default c3 c2 c2cube)
+#                                             trace + pmc: the end-of-round evidence
+#   bash tools/gpu.sh slots [OPTIONS]         the C3 launch on eleven 25 GB buffers as the
+#                                             bench allocates them (tools/slot_counters.py):
+#                                             timing, then the TLB and L2->DRAM write-path
+#                                             counters, one --pmc pass each
+#   bash tools/gpu.sh match [bench args]      the c2match line (cube + assignment + select)
+#                                             and its kernel trace
 #   AB_LIBS="a.so b.so" bash tools/gpu.sh ab CMD...
 #                                             in-tree library builds (MVM_LIB_PATH) timed by
 #                                             CMD in alternating processes, AB_ROUNDS rounds
@@ -67,6 +75,37 @@ py)
   timeout -k 10 "$LIMIT" python -u "$T" "$@" > "$O/$N.out" 2> "$O/$N.err" \
     || fail "$T" "$O/$N.err"
   tail -40 "$O/$N.out" ;;
+final)
+  bash "$0" check || exit 1
+  for W in ${@:-c3 c2 c2cube}; do
+    bash "$0" trace "$W" || exit 1
+    bash "$0" pmc "$W" || exit 1
+  done
+  echo final ok ;;
+slots)
+  OPT=${1:+--options $1}
+  timeout -k 10 300 python -u tools/slot_counters.py --buffers 11 --rounds 3 $OPT > "$O/slots.log" 2>&1 \
+    || fail slots "$O/slots.log"
+  i=0
+  for P in "TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum" \
+           "TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum TCC_EA0_WRREQ_LEVEL_sum" \
+           "GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    timeout -s KILL 240 rocprofv3 --pmc $P --output-format csv -d "$O/slots_pmc_$i" -o run -- \
+      python tools/slot_counters.py --buffers 11 --rounds 2 $OPT > "$O/slots_pmc_$i.log" 2>&1 \
+      || fail "slots pmc $i" "$O/slots_pmc_$i.log"
+    python tools/slot_counters.py --summarise "$O/slots_pmc_$i/run_counter_collection.csv" --buffers 11 \
+      > "$O/slots_pmc_$i.summary.txt" 2>&1 || true
+  done
+  echo slots ok ;;
+match)
+  timeout -k 10 "$LIMIT" python -u bench.py --workload c2match "$@" > "$O/bench_c2match.json" \
+    2> "$O/bench_c2match.err" || fail "bench c2match" "$O/bench_c2match.err"
+  # last: the profiler's teardown has crashed after writing its files
+  timeout -k 10 "$LIMIT" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_c2match" \
+    -o run -- python -u bench.py --workload c2match --cpu-seconds 0 "$@" > "$O/trace_c2match.json" \
+    2> "$O/trace_c2match.err"
+  rc=$?; echo "match trace rc=$rc (run it last: nothing after a crashed process)"; exit $rc ;;
 ab)
   for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
     for lib in $AB_LIBS; do
