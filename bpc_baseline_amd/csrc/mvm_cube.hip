@@ -1483,13 +1483,22 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         // rows in every wave instruction; 3 k per lane where the view fits
         // them (<= 48 / 96 / 192 at four / two / one rows per instruction)
         const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
-        const int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
+        int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
+        if (o.cube_cols_per_lane == 3) {
+            // 3 k per lane forced: fewer rows per instruction until a row's
+            // 64 / split lanes hold the view (unless those are forced too);
+            // views of more than 256 run the k-chunked kernel, 4 k per lane only
+            if (max_n > kChunk)
+                return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane 3: views of %d detections "
+                                "take the k-chunked kernel (4 k per lane)", (int)max_n);
+            while (split > 1 && max_n > 3 * (kWave / split) && !o.cube_rows_per_instr) split /= 2;
+            if (max_n > 3 * (kWave / split))
+                return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
+                                "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
+                                (int)max_n, 3 * (kWave / split));
+        }
         const int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane
                                              : (max_n <= 3 * (kWave / split) ? 3 : 4);
-        if (max_n <= kChunk && kpl == 3 && max_n > 3 * (kWave / split))
-            return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
-                            "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
-                            (int)max_n, 3 * (kWave / split));
         // views of 33-48 at four rows per instruction and 3 k per lane: tiles
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty

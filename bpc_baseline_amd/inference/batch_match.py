@@ -24,6 +24,8 @@ Results equal, capture by capture, the reference's ``_match`` outputs fed with
 """
 from __future__ import annotations
 
+import threading
+import weakref
 from dataclasses import dataclass
 from typing import Iterable, Iterator, List, Optional, Sequence
 
@@ -161,22 +163,39 @@ def _rig_inputs(batch: Sequence):
             np.asarray(RTs, dtype=np.float64).reshape(S, 3, 4, 4))
 
 
-_POOL = {}
+_TLS = threading.local()
+
+
+class _ThreadPools:
+    """One thread's RigWorkers by size.  Its finalizer closes them when the
+    thread ends (its thread-local storage, the only strong reference to this
+    holder, is released) or at interpreter exit, whichever comes first: a
+    service that starts a thread per request does not accumulate worker
+    processes or shared-memory slots."""
+
+    def __init__(self):
+        self.by_n = {}
+        weakref.finalize(self, _ThreadPools._close_all, self.by_n)
+
+    @staticmethod
+    def _close_all(by_n):
+        for pool in list(by_n.values()):
+            pool.close()
+        by_n.clear()
 
 
 def rig_worker_pool(n: int):
     """The calling thread's ``RigWorkers`` of ``n`` processes (started on first
-    use, reused by every stream of that thread, closed at exit).  Per thread:
-    a pool has one job in flight, and two threads streaming at once must not
-    share it."""
-    import threading
+    use, reused by every stream of that thread, closed when the thread ends or
+    at exit).  Per thread: a pool has one job in flight, and two threads
+    streaming at once must not share it."""
     from .rig_workers import RigWorkers
-    key = (threading.get_ident(), n)
-    pool = _POOL.get(key)
-    if pool is None or not pool.procs:      # first use, or closed (thread ids are reused)
-        import atexit
-        pool = _POOL[key] = RigWorkers(n)
-        atexit.register(pool.close)
+    holder = getattr(_TLS, "pools", None)
+    if holder is None:
+        holder = _TLS.pools = _ThreadPools()
+    pool = holder.by_n.get(n)
+    if pool is None or not pool.procs:      # first use, or closed
+        pool = holder.by_n[n] = RigWorkers(n)
     return pool
 
 

@@ -462,6 +462,12 @@ def pairwise_residual_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: Pai
         minval = torch.empty(plan.n_rows, dtype=torch.float32, device=dev)
     else:
         dist, argmin, minval = out
+    if not (options or {}).get("pairwise_xcd_fronts"):
+        # the library's default front count is sized from the padded bound
+        # (scenes x pairs x max rows x max columns); the plan knows the bytes
+        # this launch really writes: 4 fronts per XCD from 8 GB
+        options = dict(options or {})
+        options["pairwise_xcd_fronts"] = 4 if (dist.numel() and 4.0 * plan.dist_size >= 8e9) else 1
     torch.ops.mvmatch.pairwise_residual_argmin_out(
         pts, cam_offs, F, plan.pair_a, plan.pair_b, plan.n_scenes, plan.n_cams, plan.max_n,
         plan.dist_offs, plan.row_offs, dist, argmin, minval, _opts_list(options), plan.row_align)

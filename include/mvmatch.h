@@ -125,12 +125,18 @@ typedef struct mvm_options {
                                        contiguous (ABI 3) */
     int32_t cube_cols_per_lane;     /* FUSED (views <= 256): 0 default (3 where the view
                                        fits 3 k per lane: <= 48 / 96 / 192 at four / two /
-                                       one rows per instruction, else 4); 3 or 4 (ABI 4;
-                                       3 on a view that does not fit is an error) */
-    int32_t pairwise_xcd_fronts;    /* 0 default (4 when the launch writes >= 8 GB of
-                                       matrices, else 1); 1..16: each XCD writes its
-                                       eighth of the grid as this many concurrent
-                                       contiguous ranges (ABI 5) */
+                                       one rows per instruction, else 4); 3 or 4 (ABI 4).
+                                       3 lowers the rows per instruction until the view
+                                       fits; it is an error above 192, with a forced
+                                       cube_rows_per_instr the view does not fit, and
+                                       for views > 256 (the k-chunked kernel) */
+    int32_t pairwise_xcd_fronts;    /* 0 default (4 when the launch may write >= 8 GB of
+                                       matrices -- judged from the padded bound
+                                       n_scenes * n_pairs * max_n^2 * 4 B; the Python
+                                       plan passes the real size's choice -- else 1);
+                                       1..16: each XCD writes its eighth of the grid as
+                                       this many concurrent contiguous ranges (ABI 5;
+                                       +0.8-1.9% on C3, a margin of one box) */
     int32_t lsap_sparse_min_cols;   /* 0 default (4096); -1 off: problems with a long
                                        side >= this (and > the one-wave limit, <= 65536)
                                        and a short side <= 1024 are solved one workgroup

@@ -165,6 +165,16 @@ def test_options_init_and_validation(lib):
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 200, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(bad), None)
     assert st == 1 and b"exceed 192" in lib.mvm_last_error_string()
+    # ... with four rows per instruction forced on a view of 60 (> 48), and on
+    # the k-chunked kernel's views (> 256)
+    bad = _native.make_options(cube_kernel="fused", cube_rows_per_instr=4, cube_cols_per_lane=3)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 60, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(bad), None)
+    assert st == 1 and b"exceed 48" in lib.mvm_last_error_string()
+    bad = _native.make_options(cube_cols_per_lane=3)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 300, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 30, ctypes.byref(bad), None)
+    assert st == 1 and b"k-chunked" in lib.mvm_last_error_string()
     o.size = 3                                      # not a struct size
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(o), None)

@@ -286,14 +286,16 @@ def test_pairwise_argmin_only(cuda, argmin_path):
 
 # --------------------------------------------------------------- cube ----
 @pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "fused_kpl4",
-                        "fused_rows1_kpl4", "workspace", "generic"])
+                        "fused_rows1_kpl4", "fused_kpl3", "workspace", "generic"])
 def cube_path(request):
     """mvm_options of each cube kernel: the small-scene kernel (views of < 64
     detections), the fused tiled kernel (pair residuals computed in the
     prologue; up to 256, then its k-chunked form) with four / two / one
     (i, j) rows per wave instruction -- 3 k per lane where the view fits them
-    (the default), or 4 forced (kpl4) -- the tiled kernel over the fp64
-    workspace (beyond 256: the generic kernel) and the generic kernel."""
+    (the default), or 4 forced (kpl4), or 3 forced (kpl3: fewer rows per
+    instruction where the view needs them; views of <= 192 only) -- the tiled
+    kernel over the fp64 workspace (beyond 256: the generic kernel) and the
+    generic kernel."""
     return request.param, {"default": {}, "small": {"cube_kernel": "small"},
                            "fused": {"cube_kernel": "fused"},
                            "fused_rows2": {"cube_kernel": "fused", "cube_rows_per_instr": 2},
@@ -301,6 +303,7 @@ def cube_path(request):
                            "fused_kpl4": {"cube_kernel": "fused", "cube_cols_per_lane": 4},
                            "fused_rows1_kpl4": {"cube_kernel": "fused", "cube_rows_per_instr": 1,
                                                 "cube_cols_per_lane": 4},
+                           "fused_kpl3": {"cube_kernel": "fused", "cube_cols_per_lane": 3},
                            "workspace": {"cube_kernel": "workspace"},
                            "generic": {"cube_kernel": "generic"}}[request.param]
 
@@ -339,9 +342,11 @@ def test_cube_golden_mid_sizes(cuda, golden, cube_path):
     instruction; 250: rows off 16 bytes at one row per instruction), each in
     its own launch so each takes its size's kernel, on every cube path."""
     g = golden("a3b_cost_cubes_mid.npz")
-    _, opts = cube_path
+    path, opts = cube_path
     for n in g["names"]:
         p = [g[f"{n}_p{k}"] for k in (1, 2, 3)]
+        if path == "fused_kpl3" and max(len(x) for x in p) > 192:
+            continue                                  # 3 k per lane holds at most 192
         cam_offs = np.array([0, len(p[0]), len(p[0]) + len(p[1]), sum(len(x) for x in p)], np.int64)
         c, a, _ = run_cube(cuda, np.concatenate(p), cam_offs, g[f"{n}_F"], 1, options=opts)
         assert np.array_equal(_bits(c), _bits(g[f"{n}_cube"].reshape(-1))), f"cube {n}"
@@ -357,6 +362,8 @@ def test_cube_golden_mid_sizes(cuda, golden, cube_path):
                                         (4, 190, True), (5, 47, True), (3, 93, False)])
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
+    if cube_path[0] == "fused_kpl3" and n > 192:
+        pytest.skip("3 k per lane holds views of at most 192")
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
     c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S, options=cube_path[1])
     rc, ra, rm, _, _ = O.cube(b.pts, b.cam_offs, b.F, S)
@@ -427,6 +434,8 @@ def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
     kernel's full-tile loop, whose in-lane first index comes from lane masks
     (k0 ^ 1, k0 ^ 2, k0 ^ 3: every q position of the winner's lane)."""
     from bpc_baseline_amd.synth import make_scenes
+    if cube_path[0] == "fused_kpl3" and n > 192:
+        pytest.skip("3 k per lane holds views of at most 192")
     b = make_scenes(1, 3, n, seed=21)
     pts = b.pts.copy()
     _, ra, _, _, _ = O.cube(pts, b.cam_offs, b.F, 1, want_cube=False)

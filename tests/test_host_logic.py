@@ -596,9 +596,18 @@ def test_capture_stream_abandoned_then_reused(monkeypatch):
         for F in bm.match_capture_stream(batches, rig_workers=2):
             1 / 0                                   # an exception in the consumer
     assert len(list(bm.match_capture_stream(batches, rig_workers=2))) == 3
-    pools = []
-    th = threading.Thread(target=lambda: pools.append(bm.rig_worker_pool(2)))
+    # another thread gets its own pool, and the pool is closed when that
+    # thread ends (no worker processes left behind per thread)
+    seen = []
+
+    def other():
+        p = bm.rig_worker_pool(2)
+        seen.append((p, list(p.procs)))
+    th = threading.Thread(target=other)
     th.start()
     th.join()
-    assert pools[0] is not bm.rig_worker_pool(2)
-    pools[0].close()
+    import gc
+    gc.collect()
+    pool, procs = seen[0]
+    assert pool is not bm.rig_worker_pool(2)
+    assert not pool.procs and all(pr.poll() is not None for pr in procs)
