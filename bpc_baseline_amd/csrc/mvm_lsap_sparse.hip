@@ -384,6 +384,8 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     using KT = typename K::T;
     constexpr int kQ = kSpMaxCols / kSpBlock / 64;         // block keys per lane (32)
     __shared__ int32_t s_cand[kSpNT / 64][kSpLCap];
+    __shared__ int32_t s_grp[kSpNT / 64][kSpLCap];
+    constexpr int kWaveLanes = 64;
     const int p = (int)(blockIdx.x / kSpRowGroups), grp = (int)(blockIdx.x % kSpRowGroups);
     if (p >= n) return;
     const int64_t R = a.dims[2 * p], Kd = a.dims[2 * p + 1];
@@ -430,35 +432,75 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             thr = lo;
             theta = K::val(thr);
         }
-        int ncand = 0;                                     // candidate blocks (uniform)
+        // candidate blocks (uniform count): every block holding a cost <= theta
+        const bool groups8 = seg0 && a.bmin8;              // refine them to 8-column groups
+        int ncand = 0;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
             const bool c = k[q] <= thr && lane + 64 * q < nb;
             const uint64_t m = __ballot(c);
             if (c) {
                 const int pos = ncand + sp_mbcnt(m);
-                if (pos < kSpLCap) {                        // the block's first column | its width << 16
-                    int jt;
-                    const int g = sp_div(lane + 64 * q, bps, rbps, jt);
-                    const int j0 = g * seg + jt * kSpBlock;
-                    s_cand[wave][pos] = j0 | (min(kSpBlock, seg - jt * kSpBlock) << 16);
+                if (pos < kSpLCap) {
+                    if (groups8) {                          // the block index
+                        s_cand[wave][pos] = lane + 64 * q;
+                    } else {                                // its first column | its width << 16
+                        int jt;
+                        const int g = sp_div(lane + 64 * q, bps, rbps, jt);
+                        s_cand[wave][pos] = (g * seg + jt * kSpBlock) | (min(kSpBlock, seg - jt * kSpBlock) << 16);
+                    }
                 }
             }
             ncand += __popcll(m);
         }
         __builtin_amdgcn_wave_barrier();
-        int cnt = kSpLCap + 1;                             // every candidate block holds an entry
-        if (ncand <= kSpLCap) {
+        // the cube's 8-row minima tell which of a candidate block's four
+        // 8-column groups hold a cost <= theta (one key read per group): the
+        // gather below then reads those groups only, ~a quarter of the columns
+        int nent = ncand, eshift = 5;                      // entries, and log2 of lanes per entry
+        int32_t *ent = s_cand[wave];
+        if (groups8 && ncand <= kSpLCap) {
+            const int bps8 = (seg + 7) / 8;
+            const uint32_t *B8 = a.bmin8 + a.bmin8_offs[p];
+            int ng = 0;
+            for (int m0 = 0; m0 < ncand; m0 += 16) {      // 16 blocks x 4 groups per pass
+                const int idx = m0 + (lane >> 2), u = lane & 3;
+                bool c = false;
+                int e = 0;
+                if (idx < ncand) {
+                    int jt;
+                    const int g = sp_div(s_cand[wave][idx], bps, rbps, jt);
+                    const int g8 = 4 * jt + u;
+                    if (g8 < bps8) {
+                        c = (KT)B8[(int64_t)(g * bps8 + g8) * S + s] <= thr;
+                        e = (g * seg + 8 * g8) | (min(8, seg - 8 * g8) << 16);
+                    }
+                }
+                const uint64_t m = __ballot(c);
+                if (c) {
+                    const int pos = ng + sp_mbcnt(m);
+                    if (pos < kSpLCap) s_grp[wave][pos] = e;
+                }
+                ng += __popcll(m);
+            }
+            __builtin_amdgcn_wave_barrier();
+            nent = ng;                                     // every group listed holds an entry
+            eshift = 3;
+            ent = s_grp[wave];
+        }
+        int cnt = kSpLCap + 1;
+        if (nent <= kSpLCap) {
             cnt = 0;
-            for (int m0 = 0; m0 < ncand; m0 += 16) {       // two blocks per load, 8 loads in flight
+            const int per = kWaveLanes >> eshift, emask = (1 << eshift) - 1;   // entries per wave load
+            for (int m0 = 0; m0 < nent; m0 += 8 * per) {   // 8 loads in flight
                 CT val[8];
                 int col[8];
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
-                    const int idx = m0 + 2 * u + (lane >> 5);
-                    const int cb = idx < ncand ? s_cand[wave][idx] : 0;
-                    const int j = (cb & 0xFFFF) + (lane & 31);
-                    col[u] = (lane & 31) < (cb >> 16) ? j : -1;
+                    const int idx = m0 + u * per + (lane >> eshift);
+                    const int cb = idx < nent ? ent[idx] : 0;
+                    const int j = (cb & 0xFFFF) + (lane & emask);
+                    col[u] = (lane & emask) < (cb >> 16) ? j : -1;
                     val[u] = col[u] >= 0 ? sp_w(C0, tr, S, L, s, j) : (CT)0;
                 }
 #pragma unroll
