@@ -10,7 +10,8 @@ with every O(n) and larger step on the GPU:
   1. mvm_pack_detections      boxes/conf/cls -> half-integer centroids (CSR)
   2. host                     F (batched, bit-equal to compute_fundamental_matrix)
                               and P = K @ RT[:3]; O(1) per capture
-  3. mvm_triplet_cost_argmin  the (N, M, P) cube of every capture
+  3. mvm_triplet_cost_argmin  the (N, M, P) cube of every capture (+ its 8-row
+                              minima when an assignment is large: _bmin8)
   4. mvm_lsap_solve           scipy-identical assignment of every flattened cube
   5. mvm_select_triangulate   cost < threshold, stable sort by cost, DLT
 
@@ -130,14 +131,20 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     mark("counts D2H")
 
     plan = ops.TripletPlan(cam_offs_host, S, device=dev)
-    mark("cube plan")
-    cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan)
-    mark("cube")
     c3 = counts_host.reshape(S, 3)
+    # flattened cubes of >= 4096 rows go to the candidate-list assignment:
+    # the cube kernel then also writes the 8-row minima it reduces
+    bm8 = None
+    if S and int((c3[:, 0] * c3[:, 1]).max()) >= 4096:
+        bm8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int32, device=dev)
+    mark("cube plan")
+    cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan, bmin8=bm8)
+    mark("cube")
     lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
     mark("lsap plan")
-    row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(cube, plan.cube_offs[:-1].contiguous(),
-                                                                lplan)
+    row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(
+        cube, plan.cube_offs[:-1].contiguous(), lplan,
+        bmin8=(bm8, plan.bmin8_offs, plan.segs) if bm8 is not None else None)
     mark("lsap")
     match, cost, X, count = ops.select_triangulate(cube, plan.cube_offs, cam_offs, lplan.out_offs,
                                                    row_ind, col_ind, pts, proj_dev,

@@ -64,16 +64,20 @@ def _oracle_capture(boxes, conf, cls, offs, K, RT, conf_thresh, thr):
     return out
 
 
-@pytest.mark.parametrize("sizes", ["ipd", "large"])
+@pytest.mark.parametrize("sizes", ["ipd", "large", "c2"])
 def test_batch_vs_oracle_synthetic(cuda, sizes):
     """ipd: views of 0-40 detections (the small cube kernel, the one-wave
     assignment); large: 0-100 (the tiled cube kernels -- with empty views
-    among them -- and the wider assignment classes)."""
+    among them -- and the wider assignment classes, the candidate-list one
+    with the 8-row minima read back from the cube); c2: 130-256 (the fused
+    kernel writing the 8-row minima, the candidate-list assignment reducing
+    them)."""
     from bpc_baseline_amd.synth import make_capture
-    rng = np.random.default_rng(11 if sizes == "ipd" else 12)
-    S = 120 if sizes == "ipd" else 30
-    choices, probs = (([0, 1, 2, 6, 12, 24, 40], [.04, .06, .1, .3, .3, .1, .1]) if sizes == "ipd"
-                      else ([0, 1, 24, 45, 64, 100], [.1, .05, .15, .25, .25, .2]))
+    rng = np.random.default_rng({"ipd": 11, "large": 12, "c2": 13}[sizes])
+    S = {"ipd": 120, "large": 30, "c2": 5}[sizes]
+    choices, probs = {"ipd": ([0, 1, 2, 6, 12, 24, 40], [.04, .06, .1, .3, .3, .1, .1]),
+                      "large": ([0, 1, 24, 45, 64, 100], [.1, .05, .15, .25, .25, .2]),
+                      "c2": ([130, 160, 200, 256], [.25, .25, .25, .25])}[sizes]
     per_image, Ks, RTs = [], [], []
     for s in range(S):
         counts = list(rng.choice(choices, 3, p=probs))
@@ -109,7 +113,7 @@ def test_batch_vs_oracle_synthetic(cuda, sizes):
             np.testing.assert_allclose(gt, rt, rtol=DLT_RTOL, atol=DLT_ATOL)
         total += len(ref)
     assert total > 2 * S     # the synthetic objects are actually recovered
-    if sizes == "large":
+    if sizes != "ipd":
         return
     # a static rig: F and P passed in give the same results
     from bpc_baseline_amd.inference.batch_match import match_captures, projection_matrices

@@ -9,7 +9,10 @@ launch per buffer, buffer 0 first, timing each with HIP events.  Under
 order printed here (warm-up launch first), so the counter CSV maps to buffers
 by dispatch index: tools/slot_counters.py --summarise CSV.
 
-python tools/slot_counters.py [--buffers 11] [--rounds 2] [--scenes 1000]
+python tools/slot_counters.py [--buffers 11] [--rounds 2] [--scenes 1000] [--cams 4 --dets 1024]
+                              [--repeat R]   (R launches per buffer back to back: the
+                                              first after another buffer, the rest on a
+                                              buffer just written -- C2's same-buffer gap)
 python tools/slot_counters.py --summarise run_counter_collection.csv [--buffers 11]
 """
 import argparse
@@ -25,6 +28,9 @@ ap.add_argument("--rounds", type=int, default=2)
 ap.add_argument("--scenes", type=int, default=1000)
 ap.add_argument("--summarise", default=None, metavar="CSV")
 ap.add_argument("--kernel", default="pairwise_lazy_kernel")
+ap.add_argument("--cams", type=int, default=4)
+ap.add_argument("--dets", type=int, default=1024)
+ap.add_argument("--repeat", type=int, default=1)
 ap.add_argument("--options", default=None,
                 help="comma list of mvm_options fields for the launches (e.g. "
                      "pairwise_row_interleave=-1)")
@@ -63,7 +69,7 @@ from bpc_baseline_amd import ops  # noqa: E402
 from bpc_baseline_amd.synth import make_scenes  # noqa: E402
 
 dev = torch.device("cuda", 0)
-b = make_scenes(args.scenes, 4, 1024, seed=0)
+b = make_scenes(args.scenes, args.cams, args.dets, seed=0)
 plan = ops.PairwisePlan(b.cam_offs, b.n_scenes, b.n_cams, b.pairs, device=dev, row_align="auto")
 pts, co, F = (torch.from_numpy(x).to(dev) for x in (b.pts, b.cam_offs, b.F))
 am = torch.empty(plan.n_rows, dtype=torch.int32, device=dev)
@@ -83,15 +89,28 @@ print(f"{len(bufs)} buffers of {4 * plan.dist_size / 1e9:.1f} GB at "
 ops.pairwise_residual_argmin(pts, co, F, plan, out=(bufs[0], am, mv), options=opts)   # warm-up
 torch.cuda.synchronize()
 times = defaultdict(list)
+reps = defaultdict(lambda: defaultdict(list))   # buffer -> repeat index -> ms
 for rnd in range(args.rounds):
+    evs = []
     for i, buf in enumerate(bufs):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        ops.pairwise_residual_argmin(pts, co, F, plan, out=(buf, am, mv), options=opts)
-        e1.record()
-        torch.cuda.synchronize()
-        times[i].append(e0.elapsed_time(e1))
+        for r in range(args.repeat):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.pairwise_residual_argmin(pts, co, F, plan, out=(buf, am, mv), options=opts)
+            e1.record()
+            evs.append((i, r, e0, e1))
+        if args.repeat == 1:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    for i, r, e0, e1 in evs:
+        reps[i][r].append(e0.elapsed_time(e1))
+        if r == 0:
+            times[i].append(e0.elapsed_time(e1))
     print(f"round {rnd}: " + " ".join(f"{times[i][-1]:.3f}" for i in range(len(bufs))), flush=True)
+if args.repeat > 1:
+    for r in range(args.repeat):
+        print(f"repeat {r}: mean {np.mean([np.mean(reps[i][r]) for i in reps]):.4f} ms over the buffers",
+              flush=True)
 rows = {i: {"ms": float(np.mean(t)), "tb_s": nbytes / (np.mean(t) * 1e-3) / 1e12}
         for i, t in times.items()}
 ms = [r["ms"] for r in rows.values()]
