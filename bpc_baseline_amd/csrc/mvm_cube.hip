@@ -180,13 +180,27 @@ __device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q
 template <int KPL = kColsPerLane>
 __device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[KPL],
                                                bool lined) {
-    static_assert(KPL == 3 || KPL == 4, "3 or 4 k per lane");
+    static_assert(KPL >= 3 && KPL <= 8, "3 to 8 k per lane");
     if constexpr (KPL == 4) {   // rows may be only 4-byte aligned (P % 4 != 0)
         if (lined) store4_row_a4<1>(base, off, v);
         else store4_row_a4<0>(base, off, v);
-    } else {
+    } else if constexpr (KPL == 3) {
         if (lined) store3_row<1>(base, off, v);
         else store3_row<0>(base, off, v);
+    } else {   // 5-8: 16 bytes, then the lane's other 1-4 values
+        cube_row_store<4>(base, off, v, lined);
+        const float *w = v + 4;
+        const uint64_t b2 = base + off + 16;
+        if constexpr (KPL == 8) {
+            cube_row_store<4>(b2, 0, w, lined);
+        } else if constexpr (KPL == 7) {
+            cube_row_store<3>(b2, 0, w, lined);
+        } else if constexpr (KPL == 6) {
+            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[0] = w[0];
+            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[1] = w[1];
+        } else {
+            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[0] = w[0];
+        }
     }
 }
 
@@ -442,17 +456,24 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // KPL: k per lane.  3 where the view fits 3 * (64 / SPLIT) k (48 / 96 / 192):
 // a quarter fewer VALU per row step than 4 k per lane, whose last quarter of
 // lanes would hold no k there; rows are stored with `global_store_dwordx3`.
+// 5-8 (split forms only): a view of, e.g., 130 at two rows per instruction
+// with 5 k on each of a row's 32 lanes (81% of the lanes busy) instead of one
+// row per instruction with 3 k (68%): cube_lane_shape picks the form.
 template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane, bool BM8 = false>
-// 48-j tiles: 43 KB of LDS, 3 per CU; the 8-row minima at 4 k per lane need
-// more than 128 VGPRs (48 spilled at 4 workgroups per CU): 3 per CU
-__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2 : (kCubeRPW > 8 || (BM8 && KPL == 4)) ? 3 : 4)
+// 48-j tiles: 43 KB of LDS, 3 per CU; the 8-row minima at 4 k per lane and
+// 6-8 k per lane at two rows per instruction need more than 128 VGPRs (48 and
+// 14-85 spilled at 4 workgroups per CU): 3 per CU
+__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2
+                                       : (kCubeRPW > 8 || (BM8 && KPL == 4) || (SPLIT == 2 && KPL >= 6)) ? 3 : 4)
 void triplet_fused_kernel(CubeFusedArgs args) {
     static_assert(!BM8 || (SPLIT == 1 && kCubeRPW == 8), "8-row minima: one row per instruction, 8 per wave");
     constexpr bool HALF = SPLIT > 1;   // split mapping
     static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)),
                   "8 or 12 rows in 2 or 4 groups");
     static_assert(kCubeRPW % SPLIT == 0, "whole rows per lane group");
-    static_assert(KPL == 3 || KPL == kColsPerLane, "3 or 4 k per lane");
+    static_assert(KPL >= 3 && KPL <= 8 && (KPL <= 4 || (SPLIT > 1 && !BM8)),
+                  "3 or 4 k per lane; 5-8 in the split forms (views of 65-256 at 2 or 4 rows per "
+                  "instruction)");
     constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
     constexpr int kLPR = kWave / SPLIT;           // lanes per row
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
@@ -1434,8 +1455,8 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         o.cube_rows_per_instr != 4)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_rows_per_instr %d not 0, 1, 2 or 4",
                         (int)o.cube_rows_per_instr);
-    if (o.cube_cols_per_lane != 0 && o.cube_cols_per_lane != 3 && o.cube_cols_per_lane != 4)
-        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d not 0, 3 or 4",
+    if (o.cube_cols_per_lane != 0 && (o.cube_cols_per_lane < 3 || o.cube_cols_per_lane > 8))
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d not 0 or 3..8",
                         (int)o.cube_cols_per_lane);
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
     if (!pts_dev || !cam_offs_dev || !F_dev || !row_offs_dev)
@@ -1497,8 +1518,35 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
                                 "cube_cols_per_lane 3: views of %d detections exceed %d k per row",
                                 (int)max_n, 3 * (kWave / split));
         }
-        const int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane
-                                             : (max_n <= 3 * (kWave / split) ? 3 : 4);
+        int kpl = o.cube_cols_per_lane ? o.cube_cols_per_lane : (max_n <= 3 * (kWave / split) ? 3 : 4);
+        if (o.cube_cols_per_lane >= 5) {
+            // 5-8 k per lane forced: the split forms only (2 or 4 rows per
+            // instruction), the most rows per instruction whose lanes hold the view
+            if (max_n > kChunk)
+                return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d: views of %d detections "
+                                "take the k-chunked kernel (4 k per lane)", kpl, (int)max_n);
+            split = 0;
+            for (int sp = 4; sp >= 2 && !split; sp /= 2)
+                if ((!o.cube_rows_per_instr || o.cube_rows_per_instr == sp) && (kWave / sp) * kpl >= max_n)
+                    split = sp;
+            if (!split)
+                return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d: no 2 or 4 rows per "
+                                "instruction hold views of %d detections", kpl, (int)max_n);
+        } else if (!o.cube_cols_per_lane && !o.cube_rows_per_instr && max_n <= kChunk) {
+            // a split form with 5-8 k per lane when it keeps >= 8 % more of the
+            // lanes busy than the 3 / 4 k shape (e.g. 130: 2 rows x 5 k, 81%,
+            // against 1 row x 3 k, 68%; 100: 4 rows x 7 k, 89%, against 78%)
+            double best = (double)max_n / ((kWave / split) * kpl);
+            for (int sp = 4; sp >= 2; sp /= 2) {
+                const int lpr = kWave / sp, k = (max_n + lpr - 1) / lpr;
+                const double u = (double)max_n / (lpr * k);
+                if (k >= 5 && k <= 8 && u >= best + 0.08) {
+                    best = u;
+                    split = sp;
+                    kpl = k;
+                }
+            }
+        }
         // views of 33-48 at four rows per instruction and 3 k per lane: tiles
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty
@@ -1516,12 +1564,24 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
             return mvm_check_launch("triplet_fused_chunked_kernel");
         }
         if (split == 4) {
-            if (j48) triplet_fused_kernel<16, 12, 4, 3><<<grid, block, 0, s>>>(c);
-            else if (kpl == 3) triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c);
-            else triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c);
+            switch (j48 ? 0 : kpl) {
+            case 0: triplet_fused_kernel<16, 12, 4, 3><<<grid, block, 0, s>>>(c); break;
+            case 3: triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c); break;
+            case 4: triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c); break;
+            case 5: triplet_fused_kernel<16, 8, 4, 5><<<grid, block, 0, s>>>(c); break;
+            case 6: triplet_fused_kernel<16, 8, 4, 6><<<grid, block, 0, s>>>(c); break;
+            case 7: triplet_fused_kernel<16, 8, 4, 7><<<grid, block, 0, s>>>(c); break;
+            default: triplet_fused_kernel<16, 8, 4, 8><<<grid, block, 0, s>>>(c); break;
+            }
         } else if (split == 2) {
-            if (kpl == 3) triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c);
-            else triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c);
+            switch (kpl) {
+            case 3: triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c); break;
+            case 4: triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c); break;
+            case 5: triplet_fused_kernel<16, 8, 2, 5><<<grid, block, 0, s>>>(c); break;
+            case 6: triplet_fused_kernel<16, 8, 2, 6><<<grid, block, 0, s>>>(c); break;
+            case 7: triplet_fused_kernel<16, 8, 2, 7><<<grid, block, 0, s>>>(c); break;
+            default: triplet_fused_kernel<16, 8, 2, 8><<<grid, block, 0, s>>>(c); break;
+            }
         } else if (bmin8_dev) {                  // the 8-row minima from the same kernel
             if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3, true><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8, 1, kColsPerLane, true><<<grid, block, 0, s>>>(c);

@@ -125,10 +125,14 @@ typedef struct mvm_options {
                                        contiguous (ABI 3) */
     int32_t cube_cols_per_lane;     /* FUSED (views <= 256): 0 default (3 where the view
                                        fits 3 k per lane: <= 48 / 96 / 192 at four / two /
-                                       one rows per instruction, else 4); 3 or 4 (ABI 4).
+                                       one rows per instruction, else 4; then 5-8 k per
+                                       lane at four or two rows per instruction where
+                                       that keeps >= 8% more lanes busy, ABI 6); 3..8.
                                        3 lowers the rows per instruction until the view
-                                       fits; it is an error above 192, with a forced
-                                       cube_rows_per_instr the view does not fit, and
+                                       fits; 5-8 take the most rows per instruction
+                                       (4 or 2) that hold the view; an error where no
+                                       shape holds it (3: > 192; 5-8: > 32 k) or with a
+                                       forced cube_rows_per_instr it does not fit, and
                                        for views > 256 (the k-chunked kernel) */
     int32_t pairwise_xcd_fronts;    /* 0 default (4 when the launch may write >= 8 GB of
                                        matrices -- judged from the padded bound

@@ -285,17 +285,24 @@ def test_pairwise_argmin_only(cuda, argmin_path):
 
 
 # --------------------------------------------------------------- cube ----
+# largest view each forced lane shape holds (3 k: 192 at one row per
+# instruction; 5 k: 160 at two; 8 k at two rows: 256)
+KPL_MAX_VIEW = {"fused_kpl3": 192, "fused_kpl5": 160, "fused_rows2_kpl8": 256}
+
+
 @pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "fused_kpl4",
-                        "fused_rows1_kpl4", "fused_kpl3", "workspace", "generic"])
+                        "fused_rows1_kpl4", "fused_kpl3", "fused_kpl5", "fused_rows2_kpl8", "workspace",
+                        "generic"])
 def cube_path(request):
     """mvm_options of each cube kernel: the small-scene kernel (views of < 64
     detections), the fused tiled kernel (pair residuals computed in the
     prologue; up to 256, then its k-chunked form) with four / two / one
     (i, j) rows per wave instruction -- 3 k per lane where the view fits them
     (the default), or 4 forced (kpl4), or 3 forced (kpl3: fewer rows per
-    instruction where the view needs them; views of <= 192 only) -- the tiled
-    kernel over the fp64 workspace (beyond 256: the generic kernel) and the
-    generic kernel."""
+    instruction where the view needs them; views of <= 192 only), or 5 / 8
+    forced (the split forms' wide lanes: views of <= 160 / <= 256) -- the
+    tiled kernel over the fp64 workspace (beyond 256: the generic kernel) and
+    the generic kernel."""
     return request.param, {"default": {}, "small": {"cube_kernel": "small"},
                            "fused": {"cube_kernel": "fused"},
                            "fused_rows2": {"cube_kernel": "fused", "cube_rows_per_instr": 2},
@@ -304,6 +311,9 @@ def cube_path(request):
                            "fused_rows1_kpl4": {"cube_kernel": "fused", "cube_rows_per_instr": 1,
                                                 "cube_cols_per_lane": 4},
                            "fused_kpl3": {"cube_kernel": "fused", "cube_cols_per_lane": 3},
+                           "fused_kpl5": {"cube_kernel": "fused", "cube_cols_per_lane": 5},
+                           "fused_rows2_kpl8": {"cube_kernel": "fused", "cube_rows_per_instr": 2,
+                                                "cube_cols_per_lane": 8},
                            "workspace": {"cube_kernel": "workspace"},
                            "generic": {"cube_kernel": "generic"}}[request.param]
 
@@ -345,8 +355,8 @@ def test_cube_golden_mid_sizes(cuda, golden, cube_path):
     path, opts = cube_path
     for n in g["names"]:
         p = [g[f"{n}_p{k}"] for k in (1, 2, 3)]
-        if path == "fused_kpl3" and max(len(x) for x in p) > 192:
-            continue                                  # 3 k per lane holds at most 192
+        if max(len(x) for x in p) > KPL_MAX_VIEW.get(path, 1 << 30):
+            continue                                  # views the forced lane shape cannot hold
         cam_offs = np.array([0, len(p[0]), len(p[0]) + len(p[1]), sum(len(x) for x in p)], np.int64)
         c, a, _ = run_cube(cuda, np.concatenate(p), cam_offs, g[f"{n}_F"], 1, options=opts)
         assert np.array_equal(_bits(c), _bits(g[f"{n}_cube"].reshape(-1))), f"cube {n}"
@@ -362,8 +372,8 @@ def test_cube_golden_mid_sizes(cuda, golden, cube_path):
                                         (4, 190, True), (5, 47, True), (3, 93, False)])
 def test_cube_synthetic_vs_oracle(cuda, S, n, ragged, cube_path):
     from bpc_baseline_amd.synth import make_scenes
-    if cube_path[0] == "fused_kpl3" and n > 192:
-        pytest.skip("3 k per lane holds views of at most 192")
+    if n > KPL_MAX_VIEW.get(cube_path[0], 1 << 30):
+        pytest.skip("views the forced lane shape cannot hold")
     b = make_scenes(S, 3, n, seed=7 * n + S, ragged=ragged)
     c, a, m = run_cube(cuda, b.pts, b.cam_offs, b.F, S, options=cube_path[1])
     rc, ra, rm, _, _ = O.cube(b.pts, b.cam_offs, b.F, S)
@@ -434,8 +444,8 @@ def test_cube_row_minimum_ties_across_chunks(cuda, cube_path, n):
     kernel's full-tile loop, whose in-lane first index comes from lane masks
     (k0 ^ 1, k0 ^ 2, k0 ^ 3: every q position of the winner's lane)."""
     from bpc_baseline_amd.synth import make_scenes
-    if cube_path[0] == "fused_kpl3" and n > 192:
-        pytest.skip("3 k per lane holds views of at most 192")
+    if n > KPL_MAX_VIEW.get(cube_path[0], 1 << 30):
+        pytest.skip("views the forced lane shape cannot hold")
     b = make_scenes(1, 3, n, seed=21)
     pts = b.pts.copy()
     _, ra, _, _, _ = O.cube(pts, b.cam_offs, b.F, 1, want_cube=False)
