@@ -407,8 +407,11 @@ struct CubeFusedArgs {
     const int64_t *bmin8_offs;
 };
 
-// order-preserving key of a cube value (>= +0, +inf or NaN) for bmin8
-constexpr uint32_t kBm8NaN = 0xFFFFFFFEu;
+// order-preserving key of a cube value (>= +0 or +inf) for bmin8; NaN -> 0,
+// below every value's key, so one NaN entry shows in its group's minimum
+// (scipy rejects a cost with any NaN; a large NaN key would hide behind the
+// group's finite entries -- a NaN j point makes one NaN row of eight)
+constexpr uint32_t kBm8NaN = 0u;
 __device__ __forceinline__ uint32_t bm8_key(float v) {
     return v != v ? kBm8NaN : (__float_as_uint(v) | 0x80000000u);
 }

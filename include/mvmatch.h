@@ -246,8 +246,8 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
  * minimum over every group of 8 consecutive j of every (i, k) (ABI 6): for
  * scene s with view sizes N, M, P, row i * ceil(M/8) + g of P uint32 keys at
  * bmin8_dev + bmin8_offs_dev[s] holds, per k, the order-preserving key
- * (float bits | 0x80000000; NaN 0xFFFFFFFE) of min over j in [8g, 8g+8) of
- * cube[i][j][k].  The fused kernel of views of 129-256 detections writes them
+ * (float bits | 0x80000000) of min over j in [8g, 8g+8) of cube[i][j][k],
+ * or 0 when any of the eight is NaN.  The fused kernel of views of 129-256 detections writes them
  * itself; every other path reads them back from the cube (cube_dev required).
  */
 int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs_dev,

@@ -14,12 +14,12 @@ pytestmark = pytest.mark.gpu
 
 
 def _keys(cube_flat: np.ndarray) -> np.ndarray:
-    """order-preserving key of each cube value (>= +0, +inf or NaN)"""
+    """order-preserving key of each cube value (>= +0 or +inf; NaN -> 0)"""
     b = cube_flat.view(np.uint32) | np.uint32(0x80000000)
-    return np.where(np.isnan(cube_flat), np.uint32(0xFFFFFFFE), b)
+    return np.where(np.isnan(cube_flat), np.uint32(0), b)
 
 
-def _run(cuda, counts, seed, options=None, nan_scene=None):
+def _run(cuda, counts, seed, options=None, nan_scene=None, nan_view=2):
     from bpc_baseline_amd import ops
     from bpc_baseline_amd.synth import make_scenes
     scenes = [make_scenes(1, 3, list(c), seed=seed + 17 * s) for s, c in enumerate(counts)]
@@ -29,7 +29,7 @@ def _run(cuda, counts, seed, options=None, nan_scene=None):
     np.cumsum(np.array(counts).reshape(-1), out=co[1:])
     if nan_scene is not None:
         pts = pts.copy()
-        pts[co[3 * nan_scene + 2]] = np.nan                  # one view-2 point of that scene
+        pts[co[3 * nan_scene + nan_view] + 5] = np.nan       # one point of that scene's view
     dev = cuda
     plan = ops.TripletPlan(co, len(counts), device=dev)
     bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int32, device=dev)
@@ -100,12 +100,15 @@ def test_assignment_from_bmin8_equals_scipy(cuda, sparse_from, counts):
         assert np.array_equal(r1[o[s]:o[s + 1]], rr) and np.array_equal(c1[o[s]:o[s + 1]], cc), (N, M, P)
 
 
-def test_assignment_from_bmin8_nan_status(cuda):
-    """A NaN centroid makes NaN cube entries: the 8-row minima carry them and
-    the assignment reports scipy's invalid-entries status for that scene only."""
+@pytest.mark.parametrize("nan_view", [0, 1, 2])
+@pytest.mark.parametrize("counts", [[(40, 160, 64)] * 3, [(20, 256, 256)] * 3])
+def test_assignment_from_bmin8_nan_status(cuda, counts, nan_view):
+    """A NaN centroid makes NaN cube entries: the 8-row minima carry them
+    (a NaN j point is one NaN row of its eight: the NaN key is the smallest)
+    and the assignment reports scipy's invalid-entries status for that scene
+    only."""
     from bpc_baseline_amd import ops
-    counts = [(40, 160, 64), (40, 160, 64), (40, 160, 64)]
-    plan, cube, bm8 = _run(cuda, counts, 4, nan_scene=1)
+    plan, cube, bm8 = _run(cuda, counts, 4, nan_scene=1, nan_view=nan_view)
     c3 = plan.counts
     lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=cuda)
     _, _, st = ops.linear_sum_assignment_batched(cube, plan.cube_offs[:-1].contiguous(), lplan,
