@@ -562,7 +562,7 @@ def run_match(args, env, wl, kernel_options):
     stream = torch.cuda.current_stream(dev)
     # the cube kernel also writes its 8-row minima, which the assignment
     # reduces instead of reading the 67 GB of cubes once more (--lsap-input cost: off)
-    bm8 = (torch.empty(max(tplan.n_bmin8, 1), dtype=torch.int32, device=dev)
+    bm8 = (torch.empty(max(tplan.n_bmin8, 1), dtype=torch.int16, device=dev)
            if args.lsap_input == "bmin8" else None)
     bm8_args = (bm8, tplan.bmin8_offs, tplan.segs) if bm8 is not None else None
 
@@ -637,7 +637,7 @@ def run_match(args, env, wl, kernel_options):
     # every cost entry once (--lsap-input cost: the floor for a solver that
     # reads the cost itself)
     cost_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
-    lsap_bytes = 4.0 * float(tplan.n_bmin8) if bm8 is not None else cost_bytes
+    lsap_bytes = 2.0 * float(tplan.n_bmin8) if bm8 is not None else cost_bytes
     stages = {"cube": (cube_ms, cb, "triplet_fused_kernel"),
               "lsap": (lsap_ms, lsap_bytes, "mvm_lsap_solve kernels"),
               "select": (sel_ms, 0.0, "select_triangulate_kernel")}

@@ -399,11 +399,13 @@ struct CubeFusedArgs {
     float *minval;
     int32_t j_blocks, i_blocks;
     // optional (BM8 instantiations): per (scene, i, group of 8 j rows) the
-    // minimum over the group of every k, as order-preserving keys (NaN ->
-    // kBm8NaN): row (i * ceil(M/8) + j/8) of P keys at bmin8 + bmin8_offs[s].
-    // The candidate-list assignment (mvm_lsap_sparse.hip) reduces these
-    // instead of reading the cube once more.
-    uint32_t *bmin8;
+    // minimum over the group of every k, as the upper 16 bits of its
+    // order-preserving key (bm8_key): row (i * ceil(M/8) + j/8) of P keys at
+    // bmin8 + bmin8_offs[s].  The candidate-list assignment
+    // (mvm_lsap_sparse.hip) reduces these instead of reading the cube once
+    // more; 16 bits are a lower bound of the minimum good to 1/128, enough to
+    // choose the candidates, whose costs it then reads exactly.
+    uint16_t *bmin8;
     const int64_t *bmin8_offs;
 };
 
@@ -416,16 +418,18 @@ __device__ __forceinline__ uint32_t bm8_key(float v) {
     return v != v ? kBm8NaN : (__float_as_uint(v) | 0x80000000u);
 }
 
-// one lane's KPL keys of an 8-row group (k = kb .. kb + KPL - 1, kvalid of them in the view)
+// one lane's KPL keys of an 8-row group (k = kb .. kb + KPL - 1, kvalid of
+// them in the view), stored as their upper halves; vec: 8-byte aligned row
 template <int KPL>
-__device__ __forceinline__ void bm8_store(uint32_t *row, int kb, int kvalid, const uint32_t (&k)[KPL],
+__device__ __forceinline__ void bm8_store(uint16_t *row, int kb, int kvalid, const uint32_t (&k)[KPL],
                                           bool vec) {
     if (KPL == 4 && vec && kvalid >= 4) {
-        *reinterpret_cast<uint4 *>(row + kb) = make_uint4(k[0], k[1], k[2], k[KPL - 1]);
+        *reinterpret_cast<uint2 *>(row + kb) = make_uint2((k[0] >> 16) | (k[1] & 0xFFFF0000u),
+                                                          (k[2] >> 16) | (k[KPL - 1] & 0xFFFF0000u));
     } else {
 #pragma unroll
         for (int q = 0; q < KPL; ++q)
-            if (q < kvalid) row[kb + q] = k[q];
+            if (q < kvalid) row[kb + q] = (uint16_t)(k[q] >> 16);
     }
 }
 
@@ -742,7 +746,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
             if constexpr (BM8) {
                 if (act_k)
                     bm8_store<KPL>(args.bmin8 + args.bmin8_offs[s] + ((int64_t)i * ((M + 7) / 8) + j0 / 8) * P,
-                                   kb, kvalid, bmk, (P & 3) == 0);
+                                   kb, kvalid, bmk, (P & 3) == 0 && (args.bmin8_offs[s] & 3) == 0);
             }
             if constexpr (HALF) {
                 // each row lies on one group of kLPR lanes: reduce inside the
@@ -860,7 +864,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 for (int q = 0; q < kColsPerLane; ++q) kk[q] = bmk[q] | 0x80000000u;
                 bm8_store<kColsPerLane>(args.bmin8 + args.bmin8_offs[s] +
                                             ((int64_t)(ib + i_stride * ii) * ((M + 7) / 8) + j0 / 8) * P,
-                                        kb, kColsPerLane, kk, true);
+                                        kb, kColsPerLane, kk, (args.bmin8_offs[s] & 3) == 0);
             }
             uint32_t mk;
             int32_t mi;
@@ -1345,7 +1349,7 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
 // that do not emit the 8-row minima themselves: one workgroup per (scene, i).
 __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t *cam_offs,
                                                                    const int64_t *cube_offs,
-                                                                   const float *cube, uint32_t *bmin8,
+                                                                   const float *cube, uint16_t *bmin8,
                                                                    const int64_t *bmin8_offs, int max_n) {
     const int s = (int)(blockIdx.x / (unsigned)max_n), i = (int)(blockIdx.x % (unsigned)max_n);
     const int64_t *co = cam_offs + 3 * (int64_t)s;
@@ -1353,12 +1357,12 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
     if (i >= N || M == 0 || P == 0) return;
     const int g8 = (M + 7) / 8;
     const float *base = cube + cube_offs[s] + (int64_t)i * M * P;
-    uint32_t *out = bmin8 + bmin8_offs[s] + (int64_t)i * g8 * P;
+    uint16_t *out = bmin8 + bmin8_offs[s] + (int64_t)i * g8 * P;
     for (int jg = 0; jg < g8; ++jg) {
         for (int k = threadIdx.x; k < P; k += kThreads) {
             uint32_t m = 0xFFFFFFFFu;
             for (int j = 8 * jg; j < min(8 * jg + 8, M); ++j) m = umin(m, bm8_key(base[(int64_t)j * P + k]));
-            out[(int64_t)jg * P + k] = m;
+            out[(int64_t)jg * P + k] = (uint16_t)(m >> 16);
         }
     }
 }
@@ -1366,7 +1370,7 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
 int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                 int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
                 const int64_t *row_offs_dev, float *cube_dev, int32_t *argmin_dev, float *minval_dev,
-                uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
+                uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
                 size_t workspace_bytes, const mvm_options *opts, hipStream_t s, bool &emitted);
 
 int grid_check(int64_t blocks) {
@@ -1408,7 +1412,7 @@ int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs
                                   const double *F_dev, int32_t n_scenes, int32_t max_n,
                                   const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                                   float *cube_dev, int32_t *argmin_dev, float *minval_dev,
-                                  uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                                  uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
                                   void *workspace_dev, size_t workspace_bytes,
                                   const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
@@ -1446,7 +1450,7 @@ namespace {
 int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                 int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
                 const int64_t *row_offs_dev, float *cube_dev, int32_t *argmin_dev, float *minval_dev,
-                uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
+                uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev, void *workspace_dev,
                 size_t workspace_bytes, const mvm_options *opts, hipStream_t s, bool &emitted) {
     mvm_options o;
     int st = mvm_resolve_options(opts, o);

@@ -66,7 +66,7 @@ struct LsapArgs {
     int32_t mreg_lo, mreg_max_cols, mreg_nr_cap;
     int32_t sparse_lo;          // > 0: long sides >= this (lsap_sparse_class) are solved by
                                 // the candidate-list kernels (mvm_lsap_sparse.hip)
-    const uint32_t *bmin8;      // optional inputs of those kernels (LsapSparseArgs)
+    const uint16_t *bmin8;      // optional inputs of those kernels (LsapSparseArgs)
     const int64_t *bmin8_offs;
     const int64_t *segs;
 };
@@ -2029,7 +2029,7 @@ int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *
                        const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
                        int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                        int64_t long_min, int64_t long_max, int64_t short_max,
-                       const uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                       const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
                        const int64_t *segs_dev, const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
     mvm_options o;

@@ -31,7 +31,7 @@ struct LsapSparseArgs {
     // written by mvm_triplet_cost_argmin_bmin8 (problem p's long side is
     // segs[p]-row segments -- a cube's M -- each cut in groups of 8 rows:
     // row g * ceil(seg/8) + j/8 of S keys at bmin8 + bmin8_offs[p])
-    const uint32_t *bmin8;
+    const uint16_t *bmin8;
     const int64_t *bmin8_offs;
     const int64_t *segs;
     int32_t tb;                   // candidate blocks per row (mvm_options.lsap_sparse_blocks)

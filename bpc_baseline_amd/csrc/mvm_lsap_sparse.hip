@@ -274,9 +274,17 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
 // ---- 1'. block minima from a cube's 8-row minima ------------------------------
 // Problem p with lsap_sparse_seg(p) = seg (a cube's M): block (g, jt) is the
 // columns g*seg + [32 jt, min(32 jt + 32, seg)), i.e. the 8-row groups 4 jt ..
-// 4 jt + 3 of segment g, whose minima mvm_triplet_cost_argmin_bmin8 wrote:
-// a few MB per problem are read instead of the whole cost.  One workgroup per
-// 64 blocks; NaN / -inf keys flag the problem.
+// 4 jt + 3 of segment g, whose minima mvm_triplet_cost_argmin_bmin8 wrote as
+// 16-bit keys (the upper half of the 32-bit key: a lower bound h << 16 of the
+// minimum, which is at most (h << 16) | 0xFFFF): 2 B per 8 cost entries are
+// read instead of the whole cost.  bm receives that UPPER bound (+inf's key
+// at most), so theta = the tb-th smallest over the lanes is still a cost that
+// >= tb blocks reach; sp_lists_kernel tests candidates with the lower bound.
+// One workgroup per 64 blocks; NaN keys (0) flag the problem.
+__device__ __forceinline__ uint32_t sp_b8_upper(uint32_t h) {
+    return min((h << 16) | 0xFFFFu, 0xFF800000u);
+}
+
 __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a, int32_t n) {
     constexpr int kKeys = 8192;                            // 32 KiB of LDS keys per pass
     constexpr int kTiles = kSpMaxBlocks / 64;
@@ -296,17 +304,17 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
     const SpLayout y = lsap_sparse_layout(S, L, sizeof(float));
     unsigned char *ws = a.ws + a.ws_offs[p];
     uint32_t *bm = reinterpret_cast<uint32_t *>(ws + y.bm);
-    const uint32_t *B8 = a.bmin8 + a.bmin8_offs[p];
+    const uint16_t *B8 = a.bmin8 + a.bmin8_offs[p];
     int bp = 64;
     while (bp > 1 && S * bp > kKeys) bp >>= 1;
     const int t = threadIdx.x;
-    const int G = S / 4;
-    const bool fast = S % 4 == 0 && kSpNT % G == 0 && ((reinterpret_cast<uintptr_t>(B8)) & 15) == 0;
-    auto invalid = [](uint32_t k) { return k <= 0x007FFFFFu || k > 0xFF800000u; };   // -inf / NaN
+    const int G = S / 8;                                   // threads per group row (8 keys each)
+    const bool fast = S % 8 == 0 && kSpNT % G == 0 && ((reinterpret_cast<uintptr_t>(B8)) & 15) == 0;
+    auto invalid = [](uint32_t h) { return h < 0x8000u; };   // NaN (0); a cube holds no -inf
     int bad = 0;
     for (int pb0 = b0; pb0 < b1; pb0 += bp) {
         const int pb1 = min(pb0 + bp, b1), nrow = 4 * (pb1 - pb0);   // (block, u) rows
-        for (int x = t; x < S * bp; x += kSpNT) s_key[x] = 0xFFFFFFFFu;
+        for (int x = t; x < S * bp; x += kSpNT) s_key[x] = 0xFFFFu;
         __syncthreads();
         // local row x -> its 8-row group, or -1 past the segment's end
         auto group = [&](int x) {
@@ -315,44 +323,46 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
             return 4 * jt + u < bps8 ? g * bps8 + 4 * jt + u : -1;
         };
         if (fast) {
-            // thread: keys 4 g4 .. 4 g4 + 3 of blocks lb = t / G + q m, each
+            // thread: keys 8 g8 .. 8 g8 + 7 of blocks lb = t / G + q m, each
             // block's (up to) four 8-row groups loaded together, two blocks at
             // a time (eight 16-byte loads in flight); one thread per (key, block):
             // plain LDS stores
-            const int q = kSpNT / G, g4 = t % G, nbk = pb1 - pb0;
+            const int q = kSpNT / G, g8 = t % G, nbk = pb1 - pb0;
             for (int lb0 = t / G; lb0 < nbk; lb0 += 2 * q) {
                 uint4 v[2][4];
-                bool ok[2][4];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
                         const int lb = lb0 + h * q;
                         const int r = lb < nbk ? group(4 * lb + u) : -1;
-                        ok[h][u] = r >= 0;
-                        v[h][u] = ok[h][u] ? *reinterpret_cast<const uint4 *>(B8 + (int64_t)r * S + 4 * g4)
-                                           : make_uint4(~0u, ~0u, ~0u, ~0u);
+                        v[h][u] = r >= 0 ? *reinterpret_cast<const uint4 *>(B8 + (int64_t)r * S + 8 * g8)
+                                         : make_uint4(~0u, ~0u, ~0u, ~0u);
                     }
                 }
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int lb = lb0 + h * q;
                     if (lb >= nbk) continue;
-                    uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    // the four groups' minima per 16-bit lane of each dword
+                    uint32_t m[4];
 #pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        if (!ok[h][u]) continue;
-                        const uint4 x = v[h][u];
-                        bad |= invalid(x.x) | invalid(x.y) | invalid(x.z) | invalid(x.w);
-                        m.x = min(m.x, x.x);
-                        m.y = min(m.y, x.y);
-                        m.z = min(m.z, x.z);
-                        m.w = min(m.w, x.w);
+                    for (int d = 0; d < 4; ++d) {
+                        uint32_t lo = 0xFFFFu, hi = 0xFFFFu;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t x = d == 0 ? v[h][u].x : d == 1 ? v[h][u].y : d == 2 ? v[h][u].z : v[h][u].w;
+                            lo = min(lo, x & 0xFFFFu);
+                            hi = min(hi, x >> 16);
+                        }
+                        bad |= invalid(lo) | invalid(hi);
+                        m[d] = lo | (hi << 16);
                     }
-                    s_key[(4 * g4 + 0) * bp + lb] = m.x;
-                    s_key[(4 * g4 + 1) * bp + lb] = m.y;
-                    s_key[(4 * g4 + 2) * bp + lb] = m.z;
-                    s_key[(4 * g4 + 3) * bp + lb] = m.w;
+#pragma unroll
+                    for (int d = 0; d < 4; ++d) {
+                        s_key[(8 * g8 + 2 * d) * bp + lb] = m[d] & 0xFFFFu;
+                        s_key[(8 * g8 + 2 * d + 1) * bp + lb] = m[d] >> 16;
+                    }
                 }
             }
         } else {
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
         const int nbk = pb1 - pb0;
         for (int x = t; x < S * nbk; x += kSpNT) {
             const int sc = x / nbk, bb = x - sc * nbk;
-            bm[(int64_t)sc * nb + pb0 + bb] = s_key[sc * bp + bb];
+            bm[(int64_t)sc * nb + pb0 + bb] = sp_b8_upper(s_key[sc * bp + bb]);
         }
         __syncthreads();
     }
@@ -433,11 +443,14 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             theta = K::val(thr);
         }
         // candidate blocks (uniform count): every block holding a cost <= theta
+        // (from the cube's 16-bit minima, bm holds upper bounds: a block may
+        // hold a cost <= theta when its lower bound, the upper half, is <= thr)
         const bool groups8 = seg0 && a.bmin8;              // refine them to 8-column groups
+        const KT lowmask = groups8 ? (KT)0xFFFF0000u : ~(KT)0;
         int ncand = 0;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
-            const bool c = k[q] <= thr && lane + 64 * q < nb;
+            const bool c = (k[q] & lowmask) <= thr && lane + 64 * q < nb;
             const uint64_t m = __ballot(c);
             if (c) {
                 const int pos = ncand + sp_mbcnt(m);
@@ -461,7 +474,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         int32_t *ent = s_cand[wave];
         if (groups8 && ncand <= kSpLCap) {
             const int bps8 = (seg + 7) / 8;
-            const uint32_t *B8 = a.bmin8 + a.bmin8_offs[p];
+            const uint16_t *B8 = a.bmin8 + a.bmin8_offs[p];
             int ng = 0;
             for (int m0 = 0; m0 < ncand; m0 += 16) {      // 16 blocks x 4 groups per pass
                 const int idx = m0 + (lane >> 2), u = lane & 3;
@@ -472,7 +485,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                     const int g = sp_div(s_cand[wave][idx], bps, rbps, jt);
                     const int g8 = 4 * jt + u;
                     if (g8 < bps8) {
-                        c = (KT)B8[(int64_t)(g * bps8 + g8) * S + s] <= thr;
+                        c = ((KT)B8[(int64_t)(g * bps8 + g8) * S + s] << 16) <= thr;
                         e = (g * seg + 8 * g8) | (min(8, seg - 8 * g8) << 16);
                     }
                 }

@@ -136,7 +136,7 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     # the cube kernel then also writes the 8-row minima it reduces
     bm8 = None
     if S and int((c3[:, 0] * c3[:, 1]).max()) >= 4096:
-        bm8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int32, device=dev)
+        bm8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=dev)
     mark("cube plan")
     cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan, bmin8=bm8)
     mark("cube")

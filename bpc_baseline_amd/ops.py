@@ -191,7 +191,7 @@ def triplet_cost_bmin8_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: i
     _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
     for t, n, dt in ((cube_offs, "cube_offs", torch.int64), (row_offs, "row_offs", torch.int64),
                      (cube, "cube", torch.float32), (argmin, "argmin", torch.int32),
-                     (minval, "minval", torch.float32), (bmin8, "bmin8", torch.int32),
+                     (minval, "minval", torch.float32), (bmin8, "bmin8", torch.int16),
                      (bmin8_offs, "bmin8_offs", torch.int64), (workspace, "workspace", torch.uint8)):
         _require(t, n, dt, pts.device)
     st = _native.load().mvm_triplet_cost_argmin_bmin8(
@@ -222,7 +222,7 @@ def lsap_solve_bmin8_out(cost: Tensor, cost_offs: Tensor, dims: Tensor, ws_offs:
                      (ws_offs, "ws_offs", torch.int64), (out_offs, "out_offs", torch.int64),
                      (workspace, "workspace", torch.uint8), (row_ind, "row_ind", torch.int64),
                      (col_ind, "col_ind", torch.int64), (status, "status", torch.int32),
-                     (bmin8, "bmin8", torch.int32), (bmin8_offs, "bmin8_offs", torch.int64),
+                     (bmin8, "bmin8", torch.int16), (bmin8_offs, "bmin8_offs", torch.int64),
                      (segs, "segs", torch.int64)):
         _require(t, n, dt, dev)
     st = _native.load().mvm_lsap_solve_ex3(_p(cost), _native.MVM_F32, _p(cost_offs), _p(dims),
@@ -508,9 +508,10 @@ class TripletPlan:
         self.workspace_bytes = int(_native.load().mvm_triplet_workspace_bytes(self.n_scenes,
                                                                                self.max_n))
         # the cube's 8-row minima for the assignment (mvm_triplet_cost_argmin_bmin8):
-        # N * ceil(M/8) rows of P keys per scene
+        # N * ceil(M/8) rows of P 16-bit keys per scene, scenes 4 keys aligned
+        # (the kernel's 8-byte stores)
         bm8 = np.zeros(n_scenes + 1, np.int64)
-        np.cumsum(counts[:, 0] * ((counts[:, 1] + 7) // 8) * counts[:, 2], out=bm8[1:])
+        np.cumsum((counts[:, 0] * ((counts[:, 1] + 7) // 8) * counts[:, 2] + 3) // 4 * 4, out=bm8[1:])
         self.bmin8_offs_host = bm8
         self.n_bmin8 = int(bm8[-1])
         self.bmin8_offs, self.segs = _h2d_int64([bm8, np.ascontiguousarray(counts[:, 1])], self.device)
@@ -524,7 +525,7 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
                         options: Optional[dict] = None, bmin8: Optional[Tensor] = None):
     """-> (cube f32 [plan.n_cube], argmin i32 [plan.n_rows], minval f32 [plan.n_rows]).
     ``options``: mvm_options fields, e.g. ``{"cube_kernel": "workspace"}``.
-    ``bmin8`` (int32 [plan.n_bmin8]): also the 8-row minima that
+    ``bmin8`` (int16 [plan.n_bmin8]): also the 8-row minima that
     ``linear_sum_assignment_batched(..., bmin8=)`` reduces (needs the cube)."""
     dev = pts.device
     if out is None:

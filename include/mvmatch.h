@@ -244,17 +244,20 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
 /*
  * ... also writing, for the assignment that follows (mvm_lsap_solve_ex3), the
  * minimum over every group of 8 consecutive j of every (i, k) (ABI 6): for
- * scene s with view sizes N, M, P, row i * ceil(M/8) + g of P uint32 keys at
- * bmin8_dev + bmin8_offs_dev[s] holds, per k, the order-preserving key
- * (float bits | 0x80000000) of min over j in [8g, 8g+8) of cube[i][j][k],
- * or 0 when any of the eight is NaN.  The fused kernel of views of 129-256 detections writes them
- * itself; every other path reads them back from the cube (cube_dev required).
+ * scene s with view sizes N, M, P, row i * ceil(M/8) + g of P uint16 keys at
+ * bmin8_dev + bmin8_offs_dev[s] holds, per k, the upper 16 bits of the
+ * order-preserving key (float bits | 0x80000000) of min over j in [8g, 8g+8)
+ * of cube[i][j][k] -- a lower bound of that minimum to 1/128 -- or 0 when any
+ * of the eight is NaN.  The fused kernel of views of 129-256 detections
+ * writes them itself; every other path reads them back from the cube
+ * (cube_dev required).  Offsets that are multiples of 4 keys let the kernel
+ * store 8 bytes per lane.
  */
 int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs_dev,
                                   const double *F_dev, int32_t n_scenes, int32_t max_n,
                                   const int64_t *cube_offs_dev, const int64_t *row_offs_dev,
                                   float *cube_dev, int32_t *argmin_dev, float *minval_dev,
-                                  uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                                  uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
                                   void *workspace_dev, size_t workspace_bytes,
                                   const mvm_options *opts, mvm_stream_t stream);
 
@@ -328,7 +331,7 @@ int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *
                        const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
                        int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                        int64_t long_min, int64_t long_max, int64_t short_max,
-                       const uint32_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                       const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
                        const int64_t *segs_dev, const mvm_options *opts, mvm_stream_t stream);
 
 /*

@@ -50,17 +50,31 @@ __all__ = ["linear_sum_assignment", "candidate_lists", "DEFAULTS"]
 DEFAULTS = dict(B=32, TB=16, LCAP=128)
 
 
-def candidate_lists(W: np.ndarray, B: int, TB: int, LCAP: int):
+def _key16_upper(x: np.ndarray) -> np.ndarray:
+    """The largest float32 >= 0 whose key shares the upper 16 bits with x's
+    (x >= +0 or +inf): what the kernel takes for a block minimum it knows from
+    the cube's 16-bit keys (sp_b8_upper, capped at +inf)."""
+    k = (x.astype(np.float32).view(np.uint32) | np.uint32(0x80000000)) >> np.uint32(16)
+    up = np.minimum((k << np.uint32(16)) | np.uint32(0xFFFF), np.uint32(0xFF800000))
+    return (up & np.uint32(0x7FFFFFFF)).view(np.float32)
+
+
+def candidate_lists(W: np.ndarray, B: int, TB: int, LCAP: int, key16: bool = False):
     """Per wide row s: (cols int64 | None, beta float64 | None).
 
     cols = every column with W[s, j] <= theta_s (None: more than LCAP of
     them, the row is scanned densely); beta = the smallest value an unlisted
-    column can hold (None: no column is unlisted)."""
+    column can hold (None: no column is unlisted).  key16: theta from the
+    block minima's 16-bit key upper bounds (the kernel's input from the
+    cube's 8-row minima; float32 costs >= 0): a theta some TB blocks still
+    reach, a little above the exact rule's."""
     S, L = W.shape
     nb = -(-L // B)
     pad = np.full((S, nb * B), np.inf, W.dtype)
     pad[:, :L] = W
     bm = pad.reshape(S, nb, B).min(axis=2)
+    if key16:
+        bm = _key16_upper(bm)
     out = []
     for s in range(S):
         # the kernel's rule: lane l of a wave holds blocks l, l + 64, ...;
@@ -69,10 +83,7 @@ def candidate_lists(W: np.ndarray, B: int, TB: int, LCAP: int):
         for l in range(min(64, nb)):
             lanes[l] = bm[s, l::64].min()
         theta = np.sort(lanes)[TB - 1] if nb > TB else W.dtype.type(np.inf)
-        cand = np.nonzero(bm[s] <= theta)[0]
-        cols = (cand[:, None] * B + np.arange(B)[None, :]).reshape(-1)
-        cols = cols[cols < L]
-        cols = cols[W[s, cols] <= theta]
+        cols = np.nonzero(W[s] <= theta)[0]      # the candidate blocks' columns <= theta
         beta = None
         if not np.isinf(theta):
             beta = float(np.nextafter(W.dtype.type(theta), W.dtype.type(np.inf)))
@@ -81,7 +92,7 @@ def candidate_lists(W: np.ndarray, B: int, TB: int, LCAP: int):
 
 
 def linear_sum_assignment(cost: np.ndarray, B: int = 32, TB: int = 16, LCAP: int = 128,
-                          stats: dict | None = None):
+                          stats: dict | None = None, key16: bool = False):
     """-> (row_ind, col_ind) exactly as scipy.optimize.linear_sum_assignment."""
     cost = np.asarray(cost)
     if cost.ndim != 2:
@@ -94,7 +105,7 @@ def linear_sum_assignment(cost: np.ndarray, B: int = 32, TB: int = 16, LCAP: int
     S, L = W.shape
     if np.any(np.isnan(W)) or np.any(W == -np.inf):
         raise LsapError("matrix contains invalid numeric entries")
-    lists = candidate_lists(W, B, TB, LCAP)
+    lists = candidate_lists(W, B, TB, LCAP, key16)
     st = stats if stats is not None else {}
     for key in ("steps", "dense_min", "dense_ties", "dense_rows", "searches"):
         st.setdefault(key, 0)

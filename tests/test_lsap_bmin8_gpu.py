@@ -14,9 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _keys(cube_flat: np.ndarray) -> np.ndarray:
-    """order-preserving key of each cube value (>= +0 or +inf; NaN -> 0)"""
-    b = cube_flat.view(np.uint32) | np.uint32(0x80000000)
-    return np.where(np.isnan(cube_flat), np.uint32(0), b)
+    """upper 16 bits of the order-preserving key of each cube value (>= +0 or
+    +inf; NaN -> 0)"""
+    b = (cube_flat.view(np.uint32) | np.uint32(0x80000000)) >> np.uint32(16)
+    return np.where(np.isnan(cube_flat), np.uint32(0), b).astype(np.uint16)
 
 
 def _run(cuda, counts, seed, options=None, nan_scene=None, nan_view=2):
@@ -32,7 +33,7 @@ def _run(cuda, counts, seed, options=None, nan_scene=None, nan_view=2):
         pts[co[3 * nan_scene + nan_view] + 5] = np.nan       # one point of that scene's view
     dev = cuda
     plan = ops.TripletPlan(co, len(counts), device=dev)
-    bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int32, device=dev)
+    bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int16, device=dev)
     cube, _, _ = ops.triplet_cost_argmin(torch.from_numpy(pts).to(dev), torch.from_numpy(co).to(dev),
                                          torch.from_numpy(F).to(dev), plan, options=options, bmin8=bm8)
     return plan, cube, bm8
@@ -58,7 +59,7 @@ def test_bmin8_equals_numpy(cuda, path, batch):
     counts = BATCHES[batch]
     plan, cube, bm8 = _run(cuda, counts, 3, opts)
     c = cube.cpu().numpy()
-    got = bm8.cpu().numpy().view(np.uint32)
+    got = bm8.cpu().numpy().view(np.uint16)
     for s, (N, M, P) in enumerate(counts):
         if N * M * P == 0:
             continue

@@ -58,8 +58,9 @@ def test_model_equals_restatement_random():
     assert stats["dense_min"] > 0 and stats["dense_ties"] > 0 and stats["dense_rows"] > 0
 
 
+@pytest.mark.parametrize("key16", [False, True])
 @pytest.mark.parametrize("n", [48, 64, 100])
-def test_model_on_cubes_equals_scipy(n):
+def test_model_on_cubes_equals_scipy(n, key16):
     scipy = pytest.importorskip("scipy.optimize")
     from bpc_baseline_amd.synth import make_scenes
     from oracle import oracle as O
@@ -68,8 +69,16 @@ def test_model_on_cubes_equals_scipy(n):
     for s in range(2):
         flat = cube[s * n ** 3:(s + 1) * n ** 3].reshape(n * n, n)
         stats = {}
-        got = SP.linear_sum_assignment(flat, **SP.DEFAULTS, stats=stats)
+        got = SP.linear_sum_assignment(flat, **SP.DEFAULTS, stats=stats, key16=key16)
         ref = scipy.linear_sum_assignment(flat)
         assert _same(got, ref)
         if n >= 64:     # the lists carry the whole search: no row scanned densely
             assert stats["dense_min"] == 0 and stats["dense_ties"] == 0, stats
+
+
+def test_key16_upper_bounds():
+    """theta from 16-bit keys: an upper bound of each value within 1/128, +inf kept"""
+    x = np.array([0.0, 1e-30, 0.37, 1.0, 5e3, 3.4e38, np.inf], np.float32)
+    up = SP._key16_upper(x)
+    assert (up >= x).all() and np.isinf(up[-1])
+    assert (up[1:-1] <= x[1:-1] * (1 + 2.0 ** -7)).all()
