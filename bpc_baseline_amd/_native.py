@@ -37,7 +37,7 @@ class MvmOptions(ctypes.Structure):
         "lsap_lds_max_cols", "lsap_lds_small_cols", "lsap_mid_max_cols", "lsap_reg_max_cols",
         "lsap_reg_threads", "lsap_mreg_max_cols", "pairwise_row_interleave",
         "cube_cols_per_lane", "pairwise_xcd_fronts", "lsap_sparse_min_cols",
-        "lsap_sparse_blocks")]
+        "lsap_sparse_blocks", "cube_tile_rows")]
 
 
 OPTION_FIELDS = [n for n, _ in MvmOptions._fields_[1:]]

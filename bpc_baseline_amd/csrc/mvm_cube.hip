@@ -466,12 +466,21 @@ __device__ __forceinline__ void load_f(const double *F, double f[9]) {
 // 5-8 (split forms only): a view of, e.g., 130 at two rows per instruction
 // with 5 k on each of a row's 32 lanes (81% of the lanes busy) instead of one
 // row per instruction with 3 k (68%): cube_lane_shape picks the form.
+// workgroups per CU of triplet_fused_kernel: the VGPR budget's (more than 128
+// VGPRs for 12-row waves, the 8-row minima at 4 k per lane, and 6-8 k per
+// lane at two rows per instruction) or the static LDS's, whichever is less
+constexpr int fused_occupancy(int ib, int rpw, int split, int kpl, bool bm8) {
+    const int w13 = (kWave / split) * kpl < kChunk ? (kWave / split) * kpl : kChunk;
+    const int kj = kWaves * rpw;
+    const int lds = 8 * ib * w13 + 8 * ib * kj + 64 * (ib + kj) + 16 * (ib + kj) + 1024;
+    const int by_vgpr = (rpw > 8 || (bm8 && kpl == 4) || (split == 2 && kpl >= 6)) ? 3 : 4;
+    const int by_lds = 160 * 1024 / lds;
+    return by_lds < by_vgpr ? (by_lds > 1 ? by_lds : 1) : by_vgpr;
+}
+
 template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane, bool BM8 = false>
-// 48-j tiles: 43 KB of LDS, 3 per CU; the 8-row minima at 4 k per lane and
-// 6-8 k per lane at two rows per instruction need more than 128 VGPRs (48 and
-// 14-85 spilled at 4 workgroups per CU): 3 per CU
-__global__ __launch_bounds__(kThreads, kCubeIB > 16 ? 2
-                                       : (kCubeRPW > 8 || (BM8 && KPL == 4) || (SPLIT == 2 && KPL >= 6)) ? 3 : 4)
+// kCubeIB: i rows per tile, 16 or (split forms, mvm_options.cube_tile_rows) 32.
+__global__ __launch_bounds__(kThreads, fused_occupancy(kCubeIB, kCubeRPW, SPLIT, KPL, BM8))
 void triplet_fused_kernel(CubeFusedArgs args) {
     static_assert(!BM8 || (SPLIT == 1 && kCubeRPW == 8), "8-row minima: one row per instruction, 8 per wave");
     constexpr bool HALF = SPLIT > 1;   // split mapping
@@ -484,7 +493,12 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
     constexpr int kLPR = kWave / SPLIT;           // lanes per row
     constexpr int kJ = kWaves * kCubeRPW;                                          // j per workgroup
-    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kChunk];           // 32 KiB
+    // k columns a row's lanes hold: the e13 rows' width (a split form's view
+    // is <= kLPR * KPL, so 32 i rows at 4 rows per instruction take the LDS
+    // of 16 at one)
+    constexpr int kW13 = kLPR * KPL < kChunk ? kLPR * KPL : kChunk;
+    static_assert(kCubeIB <= kWave, "the tile's i rows: one thread of wave 0 each");
+    __shared__ __attribute__((aligned(16))) double s13[kCubeIB][kW13];             // <= 32 KiB
     __shared__ __attribute__((aligned(16))) double s12[kCubeIB][kJ];
     __shared__ LineRec s_r13[kCubeIB], s_r12[kCubeIB], s_c12[kJ], s_r23[kJ];
     __shared__ double s_p0[kCubeIB][2], s_p1[kJ][2];
@@ -548,7 +562,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
         LineRec l;
         double x, y;
     };
-    static_assert(sizeof(ColRec) * kChunk <= sizeof(s13), "F23 column scratch fits s13");
+    static_assert(sizeof(ColRec) * kW13 <= sizeof(s13), "F23 column scratch fits s13");
     ColRec *s_c23 = reinterpret_cast<ColRec *>(&s13[0][0]);
     bool any_deg = false;   // a degenerate line among this thread's (9999 sentinel)
     if (t < kCubeIB) {
@@ -603,7 +617,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
             c23.y = ky;
             any_deg |= (cl13.deg != 0.0) || (c23.l.deg != 0.0);
         }
-        s_c23[t] = c23;
+        if (t < kW13) s_c23[t] = c23;
     }
     // uniform: no line of the tile is degenerate, so every residual is
     // 0.5 * (|l1 . p1| + |l2 . p2|) without the sentinel selects
@@ -620,7 +634,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     double a23[kLaneRows][KPL];
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
-        const ColRec cl = s_c23[min(kb + q, kChunk - 1)];
+        const ColRec cl = s_c23[min(kb + q, kW13 - 1)];
 #pragma unroll
         for (int r = 0; r < kLaneRows; ++r) {
             const int rr = r + hl * kLaneRows;            // the wave row
@@ -640,7 +654,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
             s13[r][t] = e;
             tame_in &= e <= kTameResidual;
         }
-    } else {
+    } else if (t < kW13) {
         for (int r = 0; r < kCubeIB; ++r) s13[r][t] = 0.0;
     }
     for (int x = t; x < kCubeIB * kJ; x += kThreads) {
@@ -668,7 +682,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
             } else {
 #pragma unroll
-                for (int q = 0; q < KPL; ++q) a13[q] = s13[ii][min(kb + q, kChunk - 1)];
+                for (int q = 0; q < KPL; ++q) a13[q] = s13[ii][min(kb + q, kW13 - 1)];
             }
             uint32_t key[kLaneRows];
             int32_t idx[kLaneRows];
@@ -1446,6 +1460,31 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
 
 namespace {
 
+// the fused kernel at two / four rows per instruction, tiles of IB i rows
+template <int IB>
+void launch_split(int split, int kpl, bool j48, dim3 grid, dim3 block, hipStream_t s, const CubeFusedArgs &c) {
+    if (split == 4) {
+        switch (j48 ? 0 : kpl) {
+        case 0: triplet_fused_kernel<IB, 12, 4, 3><<<grid, block, 0, s>>>(c); break;
+        case 3: triplet_fused_kernel<IB, 8, 4, 3><<<grid, block, 0, s>>>(c); break;
+        case 4: triplet_fused_kernel<IB, 8, 4><<<grid, block, 0, s>>>(c); break;
+        case 5: triplet_fused_kernel<IB, 8, 4, 5><<<grid, block, 0, s>>>(c); break;
+        case 6: triplet_fused_kernel<IB, 8, 4, 6><<<grid, block, 0, s>>>(c); break;
+        case 7: triplet_fused_kernel<IB, 8, 4, 7><<<grid, block, 0, s>>>(c); break;
+        default: triplet_fused_kernel<IB, 8, 4, 8><<<grid, block, 0, s>>>(c); break;
+        }
+    } else {
+        switch (kpl) {
+        case 3: triplet_fused_kernel<IB, 8, 2, 3><<<grid, block, 0, s>>>(c); break;
+        case 4: triplet_fused_kernel<IB, 8, 2><<<grid, block, 0, s>>>(c); break;
+        case 5: triplet_fused_kernel<IB, 8, 2, 5><<<grid, block, 0, s>>>(c); break;
+        case 6: triplet_fused_kernel<IB, 8, 2, 6><<<grid, block, 0, s>>>(c); break;
+        case 7: triplet_fused_kernel<IB, 8, 2, 7><<<grid, block, 0, s>>>(c); break;
+        default: triplet_fused_kernel<IB, 8, 2, 8><<<grid, block, 0, s>>>(c); break;
+        }
+    }
+}
+
 // every cube path; `emitted`: the launched kernel wrote bmin8 itself
 int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                 int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
@@ -1465,6 +1504,8 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
     if (o.cube_cols_per_lane != 0 && (o.cube_cols_per_lane < 3 || o.cube_cols_per_lane > 8))
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d not 0 or 3..8",
                         (int)o.cube_cols_per_lane);
+    if (o.cube_tile_rows != 0 && o.cube_tile_rows != 16 && o.cube_tile_rows != 32)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_tile_rows %d not 0, 16 or 32", (int)o.cube_tile_rows);
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
     if (!pts_dev || !cam_offs_dev || !F_dev || !row_offs_dev)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
@@ -1558,8 +1599,10 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty
         const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8;
+        // i rows per tile: 32 on request in the split forms (ABI 6)
+        const int tile_rows = split > 1 && o.cube_tile_rows == 32 ? 32 : 16;
         CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
-                                     cube_dev, argmin_dev, minval_dev, max_n, 16, j48 ? 12 : 8);
+                                     cube_dev, argmin_dev, minval_dev, max_n, tile_rows, j48 ? 12 : 8);
         c.bmin8 = bmin8_dev;
         c.bmin8_offs = bmin8_offs_dev;
         const int64_t blocks = (int64_t)n_scenes * c.j_blocks * c.i_blocks;
@@ -1570,25 +1613,9 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
             triplet_fused_chunked_kernel<16, 8><<<grid, block, 0, s>>>(c);
             return mvm_check_launch("triplet_fused_chunked_kernel");
         }
-        if (split == 4) {
-            switch (j48 ? 0 : kpl) {
-            case 0: triplet_fused_kernel<16, 12, 4, 3><<<grid, block, 0, s>>>(c); break;
-            case 3: triplet_fused_kernel<16, 8, 4, 3><<<grid, block, 0, s>>>(c); break;
-            case 4: triplet_fused_kernel<16, 8, 4><<<grid, block, 0, s>>>(c); break;
-            case 5: triplet_fused_kernel<16, 8, 4, 5><<<grid, block, 0, s>>>(c); break;
-            case 6: triplet_fused_kernel<16, 8, 4, 6><<<grid, block, 0, s>>>(c); break;
-            case 7: triplet_fused_kernel<16, 8, 4, 7><<<grid, block, 0, s>>>(c); break;
-            default: triplet_fused_kernel<16, 8, 4, 8><<<grid, block, 0, s>>>(c); break;
-            }
-        } else if (split == 2) {
-            switch (kpl) {
-            case 3: triplet_fused_kernel<16, 8, 2, 3><<<grid, block, 0, s>>>(c); break;
-            case 4: triplet_fused_kernel<16, 8, 2><<<grid, block, 0, s>>>(c); break;
-            case 5: triplet_fused_kernel<16, 8, 2, 5><<<grid, block, 0, s>>>(c); break;
-            case 6: triplet_fused_kernel<16, 8, 2, 6><<<grid, block, 0, s>>>(c); break;
-            case 7: triplet_fused_kernel<16, 8, 2, 7><<<grid, block, 0, s>>>(c); break;
-            default: triplet_fused_kernel<16, 8, 2, 8><<<grid, block, 0, s>>>(c); break;
-            }
+        if (split > 1) {
+            if (tile_rows == 32) launch_split<32>(split, kpl, j48, grid, block, s, c);
+            else launch_split<16>(split, kpl, j48, grid, block, s, c);
         } else if (bmin8_dev) {                  // the 8-row minima from the same kernel
             if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3, true><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8, 1, kColsPerLane, true><<<grid, block, 0, s>>>(c);

@@ -147,6 +147,9 @@ typedef struct mvm_options {
                                        each through per-row candidate lists (ABI 6) */
     int32_t lsap_sparse_blocks;     /* 0 default (16): candidate blocks (of 32 columns)
                                        per row of that class, 1..64 (ABI 6) */
+    int32_t cube_tile_rows;         /* FUSED at two or four rows per instruction: i rows
+                                       per tile, 0 default (16), 16 or 32 (the tile's
+                                       prologue over twice the rows; ABI 6) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

@@ -179,6 +179,10 @@ def test_options_init_and_validation(lib):
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 200, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(bad), None)
     assert st == 1 and b"no 2 or 4 rows" in lib.mvm_last_error_string()
+    bad = _native.make_options(cube_tile_rows=24)
+    st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        FAKE, 1 << 20, ctypes.byref(bad), None)
+    assert st == 1 and b"cube_tile_rows" in lib.mvm_last_error_string()
     o.size = 3                                      # not a struct size
     st = lib.mvm_triplet_cost_argmin_ex(FAKE, FAKE, FAKE, 1, 4, FAKE, FAKE, FAKE, FAKE, FAKE,
                                         FAKE, 1 << 20, ctypes.byref(o), None)

@@ -287,12 +287,12 @@ def test_pairwise_argmin_only(cuda, argmin_path):
 # --------------------------------------------------------------- cube ----
 # largest view each forced lane shape holds (3 k: 192 at one row per
 # instruction; 5 k: 160 at two; 8 k at two rows: 256)
-KPL_MAX_VIEW = {"fused_kpl3": 192, "fused_kpl5": 160, "fused_rows2_kpl8": 256}
+KPL_MAX_VIEW = {"fused_kpl3": 192, "fused_kpl5": 160, "fused_rows2_kpl8": 256, "fused_tile32_kpl5": 160}
 
 
 @pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "fused_kpl4",
-                        "fused_rows1_kpl4", "fused_kpl3", "fused_kpl5", "fused_rows2_kpl8", "workspace",
-                        "generic"])
+                        "fused_rows1_kpl4", "fused_kpl3", "fused_kpl5", "fused_rows2_kpl8", "fused_tile32",
+                        "fused_tile32_kpl5", "workspace", "generic"])
 def cube_path(request):
     """mvm_options of each cube kernel: the small-scene kernel (views of < 64
     detections), the fused tiled kernel (pair residuals computed in the
@@ -300,7 +300,8 @@ def cube_path(request):
     (i, j) rows per wave instruction -- 3 k per lane where the view fits them
     (the default), or 4 forced (kpl4), or 3 forced (kpl3: fewer rows per
     instruction where the view needs them; views of <= 192 only), or 5 / 8
-    forced (the split forms' wide lanes: views of <= 160 / <= 256) -- the
+    forced (the split forms' wide lanes: views of <= 160 / <= 256), tiles of
+    32 i rows (tile32: the split forms; one row per instruction keeps 16) -- the
     tiled kernel over the fp64 workspace (beyond 256: the generic kernel) and
     the generic kernel."""
     return request.param, {"default": {}, "small": {"cube_kernel": "small"},
@@ -314,6 +315,9 @@ def cube_path(request):
                            "fused_kpl5": {"cube_kernel": "fused", "cube_cols_per_lane": 5},
                            "fused_rows2_kpl8": {"cube_kernel": "fused", "cube_rows_per_instr": 2,
                                                 "cube_cols_per_lane": 8},
+                           "fused_tile32": {"cube_kernel": "fused", "cube_tile_rows": 32},
+                           "fused_tile32_kpl5": {"cube_kernel": "fused", "cube_tile_rows": 32,
+                                                 "cube_cols_per_lane": 5},
                            "workspace": {"cube_kernel": "workspace"},
                            "generic": {"cube_kernel": "generic"}}[request.param]
 

@@ -119,7 +119,8 @@ def test_pairwise_random_vs_oracle(cuda, seed):
 CUBE_PATHS = [{}, {"cube_kernel": "small"}, {"cube_kernel": "fused"},
               {"cube_kernel": "fused", "cube_rows_per_instr": 2},
               {"cube_kernel": "fused", "cube_rows_per_instr": 1}, {"cube_kernel": "workspace"},
-              {"cube_kernel": "generic"}, {"cube_kernel": "fused", "cube_cols_per_lane": 4}]
+              {"cube_kernel": "generic"}, {"cube_kernel": "fused", "cube_cols_per_lane": 4},
+              {"cube_kernel": "fused", "cube_tile_rows": 32}]
 
 
 @pytest.mark.parametrize("seed", range(64))
