@@ -35,7 +35,8 @@ ap.add_argument("--no-check", action="store_true",
                 help="skip the bit-equality check across builds (diagnostic builds, e.g. "
                      "tools/diag cheap_lines / no_assoc patches, compute other values)")
 ap.add_argument("--scenes", type=int, default=None, help="scenes per launch (cube 250, c3 1000)")
-ap.add_argument("--dets", type=int, default=256, help="detections per view (cube)")
+ap.add_argument("--dets", default="256",
+                help="detections per view (cube): one count, or N,M,P per view")
 ap.add_argument("--alloc", default=None,
                 help="comma list of buffer kinds instead of --buffers torch buffers: "
                      "torch | vmm:MB (HIP VMM API: physical chunks of MB MiB mapped contiguously)")
@@ -117,7 +118,8 @@ for path in args.libs.split(","):
 dev = torch.device("cuda", 0)
 P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
 if args.workload == "cube":
-    b = make_scenes(args.scenes or 250, 3, args.dets, seed=0)
+    dets = [int(x) for x in args.dets.split(",")]
+    b = make_scenes(args.scenes or 250, 3, dets[0] if len(dets) == 1 else dets, seed=0)
     plan = ops.TripletPlan(b.cam_offs, b.n_scenes, device=dev)
     n_out = plan.n_cube
 else:
