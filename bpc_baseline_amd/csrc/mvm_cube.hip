@@ -180,27 +180,32 @@ __device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q
 template <int KPL = kColsPerLane>
 __device__ __forceinline__ void cube_row_store(uint64_t base, uint32_t off, const float v[KPL],
                                                bool lined) {
-    static_assert(KPL >= 3 && KPL <= 8, "3 to 8 k per lane");
+    static_assert(KPL == 3 || KPL == 4, "3 or 4 k per lane (5-8: two panels, row_store_n)");
     if constexpr (KPL == 4) {   // rows may be only 4-byte aligned (P % 4 != 0)
         if (lined) store4_row_a4<1>(base, off, v);
         else store4_row_a4<0>(base, off, v);
-    } else if constexpr (KPL == 3) {
+    } else {
         if (lined) store3_row<1>(base, off, v);
         else store3_row<0>(base, off, v);
-    } else {   // 5-8: 16 bytes, then the lane's other 1-4 values
-        cube_row_store<4>(base, off, v, lined);
-        const float *w = v + 4;
-        const uint64_t b2 = base + off + 16;
-        if constexpr (KPL == 8) {
-            cube_row_store<4>(b2, 0, w, lined);
-        } else if constexpr (KPL == 7) {
-            cube_row_store<3>(b2, 0, w, lined);
-        } else if constexpr (KPL == 6) {
-            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[0] = w[0];
-            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[1] = w[1];
-        } else {
-            reinterpret_cast<float __attribute__((address_space(1))) *>(b2)[0] = w[0];
-        }
+    }
+}
+
+// 1-4 consecutive outputs of a lane (the second panel of 5-8 k per lane)
+template <int K>
+__device__ __forceinline__ void row_store_n(uint64_t base, uint32_t off, const float *v, bool lined) {
+    static_assert(K >= 1 && K <= 4, "1 to 4 k");
+    if constexpr (K >= 3) {
+        cube_row_store<K>(base, off, v, lined);
+    } else if constexpr (K == 2) {
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        typedef f32x2 __attribute__((address_space(1), aligned(4))) g_f32x2a4;
+        const f32x2 w = {v[0], v[1]};
+        if (lined) __builtin_nontemporal_store(w, reinterpret_cast<g_f32x2a4 *>(base + off));
+        else *reinterpret_cast<g_f32x2a4 *>(base + off) = w;
+    } else {
+        typedef float __attribute__((address_space(1))) g_f32;
+        if (lined) __builtin_nontemporal_store(v[0], reinterpret_cast<g_f32 *>(base + off));
+        else *reinterpret_cast<g_f32 *>(base + off) = v[0];
     }
 }
 
@@ -509,7 +514,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     // Write order.  Dispatch puts workgroup b on XCD b % 8; the remap gives
     // each XCD a contiguous range of tiles, so one XCD holds all the tiles of
     // a scene at once.  A tile owns the i rows ib, ib + IB', ib + 2 IB', ...
-    // (IB' = i_blocks: interleaved, not 16 consecutive rows), so at its
+    // (IB' = the scene's i tile count: interleaved, not 16 consecutive rows), so at its
     // step ii the scene's tiles write the ADJACENT rows ii * IB' .. ii * IB' +
     // IB' - 1 -- one contiguous band of the cube per XCD, moving through it as
     // ii advances, instead of 16 bands 16 rows apart.
@@ -527,8 +532,11 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
     const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
     const int jw0 = jb * kJ;
-    const int i_stride = args.i_blocks;                 // tile rows: ib + i_stride * ii
-    if (jw0 >= M || ib >= N) return;                    // uniform over the workgroup
+    // tile rows: ib + i_stride * ii, over THIS scene's i tiles: a view of
+    // N < max_n rows fills ceil(N / IB) tiles (the rest exit) instead of
+    // spreading N rows thinly over all i_blocks tiles of the grid
+    const int i_stride = min(args.i_blocks, (N + kCubeIB - 1) / kCubeIB);
+    if (jw0 >= M || ib >= i_stride) return;             // uniform over the workgroup
     const int ni = min(kCubeIB, (N - ib + i_stride - 1) / i_stride);
     if (P == 0) {
         empty_k_rows(args.argmin, args.minval, args.row_offs[s], M, ib, i_stride, ni, jw0,
@@ -538,15 +546,25 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     const int j0 = jw0 + wave * kCubeRPW;
     const int nrows = min(kCubeRPW, M - j0);
     const int hl = lane / kLPR;                                      // row group of the lane
-    const int kb = KPL * (lane % kLPR);
-    const int kvalid = P - kb;
+    const int gl = lane % kLPR;                                      // lane within its row
+    // The lane's k.  3 or 4 per lane: k = KPL gl .. KPL gl + KPL - 1, one
+    // dwordx3/x4 store per row.  5-8 per lane: two panels, k = 4 gl .. 4 gl + 3
+    // (the row's first 4 kLPR k) and k = 4 kLPR + K2 gl .. (K2 = KPL - 4), so
+    // each of the row's two store instructions writes one dense contiguous
+    // span -- a lane's 5-8 consecutive k would make both sparse (16 of every
+    // 4 KPL bytes, then the rest), measured 0.59-0.70 of the write probe
+    constexpr int K2 = KPL > 4 ? KPL - 4 : 0;
+    const int kb = (K2 ? 4 : KPL) * gl;                              // the lane's first k
+    auto kpos = [&](int q) -> int {
+        if constexpr (K2 > 0) return q < 4 ? kb + q : 4 * kLPR + K2 * gl + (q - 4);
+        return kb + q;
+    };
+    const int kvalid = P - kb;                                       // 3-4 k: valid k of the lane
     const int64_t coff = args.cube_offs[s];
     const int64_t roff = args.row_offs[s];
-    // vector rows: every lane's KPL k valid or none (P % KPL == 0); 16-byte
-    // aligned for 4 k per lane (dwordx3 stores need 4 bytes)
-    // vector rows for any P: a lane stores its KPL k with one dwordx3/x4
-    // (dword-aligned: gfx950 takes it), except the one lane a row ends in
-    // when P % KPL != 0, which stores its 1..KPL-1 k alone
+    // vector rows for any P: a lane stores its k with one dwordx3/x4 per
+    // panel (dword-aligned: gfx950 takes it), except the lane a row ends in,
+    // which stores its remaining k alone
     const bool full = args.cube != nullptr;
     const bool act_k = kvalid > 0;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
@@ -634,12 +652,12 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     double a23[kLaneRows][KPL];
 #pragma unroll
     for (int q = 0; q < KPL; ++q) {
-        const ColRec cl = s_c23[min(kb + q, kW13 - 1)];
+        const ColRec cl = s_c23[min(kpos(q), kW13 - 1)];
 #pragma unroll
         for (int r = 0; r < kLaneRows; ++r) {
             const int rr = r + hl * kLaneRows;            // the wave row
             const int jj = wave * kCubeRPW + rr;
-            a23[r][q] = (rr < nrows && q < kvalid)
+            a23[r][q] = (rr < nrows && kpos(q) < P)
                             ? pair(cl.l, s_r23[jj], s_p1[jj][0], s_p1[jj][1], cl.x, cl.y)
                             : 0.0;
             tame_in &= a23[r][q] <= kTameResidual;
@@ -671,15 +689,27 @@ void triplet_fused_kernel(CubeFusedArgs args) {
     const bool tile_fast = __syncthreads_and(tame_in) != 0 && full;
     if (nrows <= 0) return;   // after the barrier: no more barriers below
 
+    // Row stores from a uniform row address: the wave's row r at step ii
+    // starts at cube + coff + ((i M + j0 + r) P) floats (scalar), and a lane
+    // of row group hl writes row r + hl * kLaneRows from its k = kb on, a
+    // loop-invariant 32-bit byte offset -- the saddr form, no per-row 64-bit
+    // address arithmetic on the VALU
+    const uint32_t lane_off = (uint32_t)((hl * kLaneRows * P + kb) * 4);
+    const uint32_t lane_off2 = (uint32_t)((hl * kLaneRows * P + (K2 ? 4 * kLPR + K2 * gl : 0)) * 4);
+    const uint64_t cube_base = reinterpret_cast<uint64_t>(args.cube) + (uint64_t)coff * 4u;
+    const bool lined = ((P | coff) & 31) == 0;
     auto main_loop = [&](auto fast_tag) {
         constexpr bool FAST = decltype(fast_tag)::value;
         for (int ii = 0; ii < ni; ++ii) {
             const int i = ib + i_stride * ii;
+            const uint64_t row_i = cube_base + (uint64_t)((int64_t)i * M + j0) * (uint64_t)P * 4u;
             double a13[KPL];
-            if constexpr (KPL == 4) {
+            if constexpr (KPL >= 4) {   // 4 k at kb (16-byte aligned), then panel 2's
                 const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
                 const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
                 a13[0] = lo.x; a13[1] = lo.y; a13[2] = hi.x; a13[3] = hi.y;
+#pragma unroll
+                for (int q = 4; q < KPL; ++q) a13[q] = s13[ii][min(kpos(q), kW13 - 1)];
             } else {
 #pragma unroll
                 for (int q = 0; q < KPL; ++q) a13[q] = s13[ii][min(kb + q, kW13 - 1)];
@@ -712,13 +742,38 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                     for (int q = 0; q < KPL; ++q) v[q] = (float)q0[q];
                     const bool whole = kvalid >= KPL;   // the lane's k all in the row
                     if (act) {
-                        if (whole) {
-                            cube_row_store<KPL>(reinterpret_cast<uint64_t>(args.cube + coff + row * P),
-                                                (uint32_t)kb * 4u, v, ((P | coff) & 31) == 0);
-                        } else {   // the row's last lane (3 k per lane, P % 3 != 0)
+                        const uint64_t row_r = row_i + (uint64_t)r * (uint64_t)P * 4u;   // uniform
+                        uint32_t off = lane_off;
+                        __asm__ volatile("" : "+v"(off));   // a 32-bit lane offset at the store: saddr form
+                        using gfloat = float __attribute__((address_space(1)));
+                        if constexpr (K2 == 0) {
+                            if (whole) {
+                                cube_row_store<KPL>(row_r, off, v, lined);
+                            } else {   // the row's last lane (P % KPL != 0)
+                                gfloat *rp = reinterpret_cast<gfloat *>(row_r + off);
 #pragma unroll
-                            for (int q = 0; q < KPL - 1; ++q)
-                                if (q < kvalid) args.cube[coff + row * P + kb + q] = v[q];
+                                for (int q = 0; q < KPL - 1; ++q)
+                                    if (q < kvalid) rp[q] = v[q];
+                            }
+                        } else {   // two panels, each one dense span per instruction
+                            if (kb + 3 < P) {
+                                cube_row_store<4>(row_r, off, v, lined);
+                            } else {
+                                gfloat *rp = reinterpret_cast<gfloat *>(row_r + off);
+#pragma unroll
+                                for (int q = 0; q < 3; ++q)
+                                    if (kb + q < P) rp[q] = v[q];
+                            }
+                            uint32_t off2 = lane_off2;
+                            __asm__ volatile("" : "+v"(off2));
+                            if (kpos(KPL - 1) < P) {
+                                row_store_n<K2>(row_r, off2, v + 4, lined);
+                            } else {
+                                gfloat *rp = reinterpret_cast<gfloat *>(row_r + off2);
+#pragma unroll
+                                for (int q = 4; q < KPL - 1; ++q)
+                                    if (kpos(q) < P) rp[q - 4] = v[q];
+                            }
                         }
                     }
                     if constexpr (BM8) {
@@ -729,7 +784,7 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                     Best b{v[0], kb};
 #pragma unroll
                     for (int q = 1; q < KPL; ++q)
-                        if (whole || q < kvalid) best_update_fast(b, v[q], kb + q);
+                        if (K2 ? kpos(q) < P : (whole || q < kvalid)) best_update_fast(b, v[q], kpos(q));
                     key[r] = act ? __float_as_uint(b.v) + 1u : kKeyInvalid;
                     idx[r] = act ? b.j : 0x7FFFFFFF;
                 } else {
@@ -746,10 +801,10 @@ void triplet_fused_kernel(CubeFusedArgs args) {
 #pragma unroll
                     for (int q = 0; q < KPL; ++q) {
                         v[q] = (float)qq[q];
-                        if (act && q < kvalid) {
+                        if (act && kpos(q) < P) {
                             if (args.cube)
-                                args.cube[coff + row * P + kb + q] = v[q];   // L2 merges the 4 strided dword stores
-                            best_update_safe(b, v[q], kb + q);
+                                args.cube[coff + row * P + kpos(q)] = v[q];   // L2 merges the strided dword stores
+                            best_update_safe(b, v[q], kpos(q));
                             if constexpr (BM8) bmk[q] = umin(bmk[q], bm8_key(v[q]));
                         }
                     }
@@ -779,9 +834,9 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 }
                 const int rr = g + hl * kLaneRows;
                 if (g < kLaneRows && rr < nrows) {
-                    const int64_t row = roff + (int64_t)i * M + j0 + rr;
-                    if (args.argmin) args.argmin[row] = (mk == kKeyInvalid) ? -1 : mi;
-                    if (args.minval) args.minval[row] = value_of_key(mk);
+                    const int64_t row0 = roff + (int64_t)i * M + j0;   // uniform
+                    if (args.argmin) (args.argmin + row0)[rr] = (mk == kKeyInvalid) ? -1 : mi;
+                    if (args.minval) (args.minval + row0)[rr] = value_of_key(mk);
                 }
             } else if constexpr (FAST && kCubeRPW == 8) {   // finite keys, one k-chunk
                 uint32_t mk;
