@@ -547,82 +547,131 @@ def run_match(args, env, wl, kernel_options):
     batch = make_scenes(n_local, 3, wl["n_dets"], seed=args.seed, first_scene=first)
     proj = projection_matrices(batch.meta["Ks"], batch.meta["RTs"])
     log(f"[rank {env.rank}] generated {n_local} scenes in {time.perf_counter() - t0:.1f}s")
-    pts = torch.from_numpy(batch.pts).to(dev)
-    cam_offs = torch.from_numpy(batch.cam_offs).to(dev)
-    F = torch.from_numpy(batch.F).to(dev)
-    proj_d = torch.from_numpy(proj).to(dev)
-    tplan = ops.TripletPlan(batch.cam_offs, n_local, device=dev)
-    c3 = tplan.counts
-    lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
-    cube = torch.empty(tplan.n_cube, dtype=torch.float32, device=dev)
-    am = torch.empty(tplan.n_rows, dtype=torch.int32, device=dev)
-    mv = torch.empty(tplan.n_rows, dtype=torch.float32, device=dev)
-    offs = tplan.cube_offs[:-1].contiguous()
     threshold = float(wl["threshold"])
+    # The step runs in chunks of scenes on two streams: the cubes one after
+    # the other on the launch stream, and each chunk's assignment + select on
+    # a second stream as soon as its cube is written, so the latency-bound
+    # assignment overlaps the HBM-bound cube of the next chunk (the cube of a
+    # chunk waits for the previous step's use of its buffers).  --match-chunks 1
+    # is the serial chain.
+    n_chunks = max(1, min(args.match_chunks, n_local))
+    bounds = np.linspace(0, n_local, n_chunks + 1).astype(np.int64)
     stream = torch.cuda.current_stream(dev)
-    # the cube kernel also writes its 8-row minima, which the assignment
-    # reduces instead of reading the 67 GB of cubes once more (--lsap-input cost: off)
-    bm8 = (torch.empty(max(tplan.n_bmin8, 1), dtype=torch.int16, device=dev)
-           if args.lsap_input == "bmin8" else None)
-    bm8_args = (bm8, tplan.bmin8_offs, tplan.segs) if bm8 is not None else None
+    side = torch.cuda.Stream(dev) if n_chunks > 1 else stream
+    chunks = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        a, b = int(a), int(b)
+        co_h = batch.cam_offs[3 * a:3 * b + 1] - batch.cam_offs[3 * a]
+        ch = {"first": a, "n": b - a, "co_h": co_h}
+        ch["pts"] = torch.from_numpy(batch.pts[batch.cam_offs[3 * a]:batch.cam_offs[3 * b]]).to(dev)
+        ch["cam_offs"] = torch.from_numpy(co_h).to(dev)
+        ch["F"] = torch.from_numpy(batch.F[3 * a:3 * b]).to(dev)
+        ch["proj"] = torch.from_numpy(np.ascontiguousarray(proj[a:b])).to(dev)
+        tp = ops.TripletPlan(co_h, b - a, device=dev)
+        c3 = tp.counts
+        ch["tplan"] = tp
+        ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+        ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
+        ch["am"] = torch.empty(tp.n_rows, dtype=torch.int32, device=dev)
+        ch["mv"] = torch.empty(tp.n_rows, dtype=torch.float32, device=dev)
+        ch["offs"] = tp.cube_offs[:-1].contiguous()
+        # the cube kernel also writes its 8-row minima, which the assignment
+        # reduces instead of reading the cubes once more (--lsap-input cost: off)
+        ch["bm8"] = (torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+                     if args.lsap_input == "bmin8" else None)
+        ch["used"] = None                   # event: the previous step's reads of the buffers
+        chunks.append(ch)
 
     def step(ev=None):
-        if ev:
-            ev[0].record(stream)
-        ops.triplet_cost_argmin(pts, cam_offs, F, tplan, out=(cube, am, mv), options=kernel_options,
-                                bmin8=bm8)
-        if ev:
-            ev[1].record(stream)
-        r, c, st = ops.linear_sum_assignment_batched(cube, offs, lplan, options=kernel_options,
-                                                     bmin8=bm8_args)
-        if ev:
-            ev[2].record(stream)
-        res = ops.select_triangulate(cube, tplan.cube_offs, cam_offs, lplan.out_offs, r, c, pts,
-                                     proj_d, threshold)
-        if ev:
-            ev[3].record(stream)
-        return (r, c, st) + tuple(res)
+        outs = []
+        cube_done = []
+        for k, ch in enumerate(chunks):
+            if ch["used"] is not None:
+                stream.wait_event(ch["used"])
+            if ev:
+                ev[k][0].record(stream)
+            ops.triplet_cost_argmin(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"],
+                                    out=(ch["cube"], ch["am"], ch["mv"]), options=kernel_options,
+                                    bmin8=ch["bm8"])
+            e = torch.cuda.Event()
+            e.record(stream)
+            cube_done.append(e)
+            if ev:
+                ev[k][1].record(stream)
+        for k, ch in enumerate(chunks):
+            side.wait_event(cube_done[k])
+            with torch.cuda.stream(side):
+                if ev:
+                    ev[k][2].record(side)
+                bm8_args = ((ch["bm8"], ch["tplan"].bmin8_offs, ch["tplan"].segs)
+                            if ch["bm8"] is not None else None)
+                r, c, st = ops.linear_sum_assignment_batched(ch["cube"], ch["offs"], ch["lplan"],
+                                                             options=kernel_options, bmin8=bm8_args)
+                if ev:
+                    ev[k][3].record(side)
+                res = ops.select_triangulate(ch["cube"], ch["tplan"].cube_offs, ch["cam_offs"],
+                                             ch["lplan"].out_offs, r, c, ch["pts"], ch["proj"],
+                                             threshold)
+                if ev:
+                    ev[k][4].record(side)
+                u = torch.cuda.Event()
+                u.record(side)
+                ch["used"] = u
+            outs.append((r, c, st) + tuple(res))
+        stream.wait_stream(side)
+        return outs
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in chunks]
+           for _ in range(args.steps)]
     env.barrier()
     torch.cuda.synchronize(dev)
     with ClockSampler(dev) as clocks:
         t_start = time.perf_counter()
-        for s in range(args.steps):
-            out = step(evs[s])
+        for s_ in range(args.steps):
+            outs = step(evs[s_])
         torch.cuda.synchronize(dev)
         env.barrier()
         elapsed = time.perf_counter() - t_start
     elapsed = max_over_ranks(env, elapsed)
-    stage = np.array([[e[0].elapsed_time(e[1]), e[1].elapsed_time(e[2]), e[2].elapsed_time(e[3])]
+    # kernel time per stage, summed over the chunks (they overlap across stages)
+    stage = np.array([[sum(e[k][0].elapsed_time(e[k][1]) for k in range(n_chunks)),
+                       sum(e[k][2].elapsed_time(e[k][3]) for k in range(n_chunks)),
+                       sum(e[k][3].elapsed_time(e[k][4]) for k in range(n_chunks))]
                       for e in evs])                          # ms per step: cube, lsap, select
     cube_ms, lsap_ms, sel_ms = (float(x) for x in stage.mean(axis=0))
-    r, c, st, match, cost, X, count = out
-    status = st.cpu().numpy()
-    count_h = count.cpu().numpy()
+    status = np.concatenate([o[2].cpu().numpy() for o in outs])
+    count_h = np.concatenate([o[6].cpu().numpy() for o in outs])
     n_matches = sum_over_ranks(env, int(count_h.sum()))
+    tplan_counts = np.concatenate([ch["tplan"].counts for ch in chunks])
+    n_bmin8 = sum(ch["tplan"].n_bmin8 for ch in chunks)
 
     # ---- parity (untimed): a few scenes against the CPU chain --------------
     parity_ok, detail = bool((status == 0).all()), []
     if env.is_root:
-        r_h, c_h = r.cpu().numpy(), c.cpu().numpy()
-        m_h, X_h = match.cpu().numpy(), X.cpu().numpy()
         picks = sorted({0, n_local // 3, (2 * n_local) // 3, n_local - 1})
         for s in picks:
+            k_ch = int(np.searchsorted(bounds, s, side="right")) - 1
+            ch, out = chunks[k_ch], outs[k_ch]
+            sl = s - ch["first"]
+            r, c, st, match, cost, X, count = out
             rc, rr, rcol, rm, rX = match_cpu_chain(batch, proj, s, threshold,
                                                    nthreads=cpu_threads())
-            o = int(tplan.cube_offs_host[s])
-            cube_ok = np.array_equal(cube[o:o + rc.size].cpu().numpy().view(np.int32), rc.view(np.int32))
-            lo = int(lplan.out_offs_host[s])
+            o = int(ch["tplan"].cube_offs_host[sl])
+            cube_ok = np.array_equal(ch["cube"][o:o + rc.size].cpu().numpy().view(np.int32),
+                                     rc.view(np.int32))
+            lo = int(ch["lplan"].out_offs_host[sl])
             nn = rr.size
-            lsap_ok = (np.array_equal(r_h[lo:lo + nn], rr) and np.array_equal(c_h[lo:lo + nn], rcol))
-            k = int(count_h[s])
-            got = [tuple(int(v) for v in m_h[lo + w]) for w in range(k)]
+            lsap_ok = (np.array_equal(r[lo:lo + nn].cpu().numpy(), rr)
+                       and np.array_equal(c[lo:lo + nn].cpu().numpy(), rcol))
+            k = int(count[sl].item())
+            m_h = match[lo:lo + k].cpu().numpy()
+            got = [tuple(int(v) for v in m_h[w]) for w in range(k)]
             match_ok = got == rm
-            x_ok = match_ok and (k == 0 or np.allclose(X_h[lo:lo + k], rX, rtol=1e-10, atol=1e-9))
+            x_ok = match_ok and (k == 0 or np.allclose(X[lo:lo + k].cpu().numpy(), rX, rtol=1e-10,
+                                                       atol=1e-9))
             parity_ok &= bool(cube_ok and lsap_ok and match_ok and x_ok)
             detail.append({"scene": first + s, "cube_bit_exact": bool(cube_ok),
                            "assignment_equal": bool(lsap_ok), "matches": k,
@@ -637,7 +686,7 @@ def run_match(args, env, wl, kernel_options):
     # every cost entry once (--lsap-input cost: the floor for a solver that
     # reads the cost itself)
     cost_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
-    lsap_bytes = 2.0 * float(tplan.n_bmin8) if bm8 is not None else cost_bytes
+    lsap_bytes = 2.0 * float(n_bmin8) if args.lsap_input == "bmin8" else cost_bytes
     stages = {"cube": (cube_ms, cb, "triplet_fused_kernel"),
               "lsap": (lsap_ms, lsap_bytes, "mvm_lsap_solve kernels"),
               "select": (sel_ms, 0.0, "select_triangulate_kernel")}
@@ -669,14 +718,18 @@ def run_match(args, env, wl, kernel_options):
                    "n_scenes_per_gpu": n_local, "n_scenes_total": total,
                    "matching_threshold": threshold, "kernel_options": kernel_options,
                    "lsap_input": args.lsap_input,
-                   "launch": "eager op calls (the assignment's launch is cooperative)",
+                   "launch": (f"eager op calls, {n_chunks} chunks of scenes: cubes on the launch "
+                              "stream, each chunk's assignment + select on a second stream once "
+                              "its cube is written" if n_chunks > 1 else "eager op calls, serial"),
+                   "match_chunks": n_chunks,
                    "parallelism": f"scene-sharded x{world}" if env.initialised else "single GPU"},
         "stages_ms": {"cube": cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
-                      "note": "rank 0, HIP events on the launch stream, mean over the timed steps"},
+                      "note": ("rank 0, HIP events on each stage's stream, summed over the chunks, "
+                               "mean over the timed steps; the stages of different chunks overlap")},
         "lsap": {"problems": n_local, "shape": f"{int(counts[0, 0] * counts[0, 1])} x {int(counts[0, 2])}",
                  "ms_per_batch": lsap_ms, "ms_per_problem": lsap_ms / max(1, n_local),
                  "streamed_gb": lsap_bytes / 1e9, "cost_gb": cost_bytes / 1e9,
-                 "input": ("the cube kernel's 8-row minima (mvm_lsap_solve_ex3)" if bm8 is not None
+                 "input": ("the cube kernel's 8-row minima (mvm_lsap_solve_ex3)" if args.lsap_input == "bmin8"
                            else "the cost cubes (mvm_lsap_solve_ex2)")},
         "matches_per_step": n_matches,
         "sclk": clocks.summary("sclk"),
@@ -739,6 +792,10 @@ def main():
                     help="mvm_options fields for the launches (include/mvmatch.h; e.g. "
                          "pairwise_row_groups=2): kernel-path choices that never change results, "
                          "for A/B runs of the line itself; recorded in config.kernel_options")
+    ap.add_argument("--match-chunks", type=int, default=1,
+                    help="c2match: scenes per step in this many chunks, the assignment of one "
+                         "overlapping the cube of the next on a second stream (1: serial, the "
+                         "default: the overlap measured slower, DESIGN §11.9)")
     ap.add_argument("--lsap-input", choices=["bmin8", "cost"], default="bmin8",
                     help="c2match: the assignment's block minima from the cube kernel's 8-row "
                          "minima (default) or from reading the cost cubes again")
