@@ -489,8 +489,9 @@ __global__ __launch_bounds__(kThreads, fused_occupancy(kCubeIB, kCubeRPW, SPLIT,
 void triplet_fused_kernel(CubeFusedArgs args) {
     static_assert(!BM8 || (SPLIT == 1 && kCubeRPW == 8), "8-row minima: one row per instruction, 8 per wave");
     constexpr bool HALF = SPLIT > 1;   // split mapping
-    static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)),
-                  "8 or 12 rows in 2 or 4 groups");
+    static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)) ||
+                      (kCubeRPW == 8 && SPLIT == 8 && KPL <= 4),
+                  "8 or 12 rows in 2 or 4 groups, or 8 rows in 8 groups of 3-4 k per lane");
     static_assert(kCubeRPW % SPLIT == 0, "whole rows per lane group");
     static_assert(KPL >= 3 && KPL <= 8 && (KPL <= 4 || (SPLIT > 1 && !BM8)),
                   "3 or 4 k per lane; 5-8 in the split forms (views of 65-256 at 2 or 4 rows per "
@@ -1249,11 +1250,13 @@ __global__ __launch_bounds__(kThreads, 3) void triplet_fused_chunked_kernel(Cube
 // wave instruction 1 KiB contiguous whatever P is -- and finally one thread
 // per (i, j) row recomputes the row from LDS for the argmin over k.
 constexpr int kSmallMaxN = 64;
-// default switch-over to the fused kernel's four-rows-per-wave form: measured
-// per 1000 scenes, small vs fused: 24^3 0.041 vs 0.064 ms, 32^3 0.095 vs
-// 0.072, 40^3 0.138 vs 0.173, 48^3 0.220 vs 0.193, 56^3 0.417 vs 0.261
-// (the fused tiles are 32 j wide: M = 40 leaves 3/8 of them empty)
-constexpr int kSmallAutoMaxN = 44;
+// default switch-over to the fused kernel: measured on 2 GB launches, the
+// same buffers (profiles/r05/cube/small/), ms per launch, small vs fused at
+// eight rows per instruction with tiles of 32 i rows (up to 32) or four rows
+// per instruction (above): 16^3 0.974 vs 1.063, 24^3 0.787 vs 0.571, 32^3
+// 1.162 vs 0.426, 40^3 0.850 vs 0.581, 44^3 0.921 vs 0.500 (round 1 had set
+// 44 against the fused kernel of its time)
+constexpr int kSmallAutoMaxN = 16;
 
 struct CubeSmallArgs {
     const double *pts;
@@ -1518,7 +1521,10 @@ namespace {
 // the fused kernel at two / four rows per instruction, tiles of IB i rows
 template <int IB>
 void launch_split(int split, int kpl, bool j48, dim3 grid, dim3 block, hipStream_t s, const CubeFusedArgs &c) {
-    if (split == 4) {
+    if (split == 8) {   // views of <= 32: eight rows per instruction
+        if (kpl == 3) triplet_fused_kernel<IB, 8, 8, 3><<<grid, block, 0, s>>>(c);
+        else triplet_fused_kernel<IB, 8, 8, 4><<<grid, block, 0, s>>>(c);
+    } else if (split == 4) {
         switch (j48 ? 0 : kpl) {
         case 0: triplet_fused_kernel<IB, 12, 4, 3><<<grid, block, 0, s>>>(c); break;
         case 3: triplet_fused_kernel<IB, 8, 4, 3><<<grid, block, 0, s>>>(c); break;
@@ -1553,8 +1559,8 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
     if (o.cube_kernel < MVM_CUBE_DEFAULT || o.cube_kernel > MVM_CUBE_GENERIC)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_kernel %d", (int)o.cube_kernel);
     if (o.cube_rows_per_instr != 0 && o.cube_rows_per_instr != 1 && o.cube_rows_per_instr != 2 &&
-        o.cube_rows_per_instr != 4)
-        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_rows_per_instr %d not 0, 1, 2 or 4",
+        o.cube_rows_per_instr != 4 && o.cube_rows_per_instr != 8)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_rows_per_instr %d not 0, 1, 2, 4 or 8",
                         (int)o.cube_rows_per_instr);
     if (o.cube_cols_per_lane != 0 && (o.cube_cols_per_lane < 3 || o.cube_cols_per_lane > 8))
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_cols_per_lane %d not 0 or 3..8",
@@ -1603,11 +1609,13 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         return mvm_check_launch("triplet_small_kernel");
     }
     if (kernel == MVM_CUBE_DEFAULT || kernel == MVM_CUBE_SMALL || kernel == MVM_CUBE_FUSED) {
-        // tiles of 16 i x 32 j; views of <= 64 / <= 128 put four / two (i, j)
-        // rows in every wave instruction; 3 k per lane where the view fits
-        // them (<= 48 / 96 / 192 at four / two / one rows per instruction)
-        const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 4;
-        int split = (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
+        // tiles of 16 (32) i x 32 j; views of <= 32 / <= 64 / <= 128 put
+        // eight / four / two (i, j) rows in every wave instruction; 3 k per
+        // lane where the view fits them (<= 24 / 48 / 96 / 192 at eight / four
+        // / two / one rows per instruction)
+        const int want = o.cube_rows_per_instr ? o.cube_rows_per_instr : 8;
+        int split = (want >= 8 && max_n <= 4 * (kWave / 8)) ? 8
+                  : (want >= 4 && max_n <= kChunk / 4) ? 4 : (want >= 2 && max_n <= kChunk / 2) ? 2 : 1;
         if (o.cube_cols_per_lane == 3) {
             // 3 k per lane forced: fewer rows per instruction until a row's
             // 64 / split lanes hold the view (unless those are forced too);
@@ -1654,8 +1662,12 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty
         const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8;
-        // i rows per tile: 32 on request in the split forms (ABI 6)
-        const int tile_rows = split > 1 && o.cube_tile_rows == 32 ? 32 : 16;
+        // i rows per tile: 32 on request in the split forms (ABI 6), and by
+        // default at eight rows per instruction (views of <= 32: a tile of
+        // 16 i rows of such a view is mostly prologue; 24^3 0.663 -> 0.571,
+        // 32^3 0.456 -> 0.426 ms per 2 GB launch)
+        const int tile_rows =
+            split > 1 && (o.cube_tile_rows == 32 || (o.cube_tile_rows == 0 && split == 8)) ? 32 : 16;
         CubeFusedArgs c = fused_args(pts_dev, cam_offs_dev, F_dev, cube_offs_dev, row_offs_dev,
                                      cube_dev, argmin_dev, minval_dev, max_n, tile_rows, j48 ? 12 : 8);
         c.bmin8 = bmin8_dev;

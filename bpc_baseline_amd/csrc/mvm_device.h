@@ -215,13 +215,15 @@ __device__ __forceinline__ void store_row_results(const uint32_t (&kmin)[RPW],
 }
 // Minimum over aligned groups of L lanes, in every lane of the group: L = 16
 // is one DPP row (quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
-// row_mirror), L = 32 joins two rows with an xor-16 swizzle.
+// row_mirror), L = 8 its first three steps, L = 32 joins two rows with an
+// xor-16 swizzle.
 template <int L>
 __device__ __forceinline__ uint32_t lane_group_min(uint32_t v) {
-    static_assert(L == 16 || L == 32, "16- or 32-lane groups");
+    static_assert(L == 8 || L == 16 || L == 32, "8-, 16- or 32-lane groups");
     v = dpp_min<0xB1>(v);
     v = dpp_min<0x4E>(v);
     v = dpp_min<0x141>(v);
+    if constexpr (L == 8) return v;
     v = dpp_min<0x140>(v);
     if constexpr (L == 32) {
         const uint32_t o = (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (16 << 10));

@@ -95,9 +95,10 @@ typedef struct mvm_options {
     int32_t pairwise_rows_per_wave; /* 0 default (16); 4, 8 or 16 */
     int32_t pairwise_row_groups;    /* 0 default (~256 rows per workgroup, ~128 for small grids); 1..16 */
     int32_t cube_kernel;            /* MVM_CUBE_* */
-    int32_t cube_rows_per_instr;    /* FUSED: 0 default (by view size); 1, 2 or 4
-                                       (i, j) rows per wave instruction, capped by
-                                       the view size (2: <= 128, 4: <= 64) */
+    int32_t cube_rows_per_instr;    /* FUSED: 0 default (by view size: 8 up to 32,
+                                       then 4 / 2 / 1); 1, 2, 4 or 8 (i, j) rows per
+                                       wave instruction, capped by the view size
+                                       (2: <= 128, 4: <= 64, 8: <= 32) */
     int32_t lsap_wave_max_cols;     /* 0 default (1024); -1 never the one-wave
                                        kernel; else a long-side limit <= 1024 */
     int32_t lsap_multi_g;           /* 0 default (auto: as many co-resident
@@ -147,9 +148,10 @@ typedef struct mvm_options {
                                        each through per-row candidate lists (ABI 6) */
     int32_t lsap_sparse_blocks;     /* 0 default (16): candidate blocks (of 32 columns)
                                        per row of that class, 1..64 (ABI 6) */
-    int32_t cube_tile_rows;         /* FUSED at two or four rows per instruction: i rows
-                                       per tile, 0 default (16), 16 or 32 (the tile's
-                                       prologue over twice the rows; ABI 6) */
+    int32_t cube_tile_rows;         /* FUSED at two, four or eight rows per
+                                       instruction: i rows per tile, 0 default (32 at
+                                       eight rows per instruction, else 16), 16 or 32
+                                       (the tile's prologue over twice the rows; ABI 6) */
 } mvm_options;
 
 /* Fill *opts with the defaults (all 0) and opts->size. */

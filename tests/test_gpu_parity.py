@@ -292,12 +292,14 @@ KPL_MAX_VIEW = {"fused_kpl3": 192, "fused_kpl5": 160, "fused_rows2_kpl8": 256, "
 
 @pytest.fixture(params=["default", "small", "fused", "fused_rows2", "fused_rows1", "fused_kpl4",
                         "fused_rows1_kpl4", "fused_kpl3", "fused_kpl5", "fused_rows2_kpl8", "fused_tile32",
-                        "fused_tile32_kpl5", "workspace", "generic"])
+                        "fused_tile32_kpl5", "fused_rows8_tile16", "fused_rows4", "workspace",
+                        "generic"])
 def cube_path(request):
     """mvm_options of each cube kernel: the small-scene kernel (views of < 64
     detections), the fused tiled kernel (pair residuals computed in the
     prologue; up to 256, then its k-chunked form) with four / two / one
-    (i, j) rows per wave instruction -- 3 k per lane where the view fits them
+    (i, j) rows per wave instruction (eight up to 32: rows8_tile16 with tiles of
+    16 i rows, the default 32; rows4 the four-row form there) -- 3 k per lane where the view fits them
     (the default), or 4 forced (kpl4), or 3 forced (kpl3: fewer rows per
     instruction where the view needs them; views of <= 192 only), or 5 / 8
     forced (the split forms' wide lanes: views of <= 160 / <= 256), tiles of
@@ -316,6 +318,9 @@ def cube_path(request):
                            "fused_rows2_kpl8": {"cube_kernel": "fused", "cube_rows_per_instr": 2,
                                                 "cube_cols_per_lane": 8},
                            "fused_tile32": {"cube_kernel": "fused", "cube_tile_rows": 32},
+                           "fused_rows8_tile16": {"cube_kernel": "fused", "cube_rows_per_instr": 8,
+                                                  "cube_tile_rows": 16},
+                           "fused_rows4": {"cube_kernel": "fused", "cube_rows_per_instr": 4},
                            "fused_tile32_kpl5": {"cube_kernel": "fused", "cube_tile_rows": 32,
                                                  "cube_cols_per_lane": 5},
                            "workspace": {"cube_kernel": "workspace"},

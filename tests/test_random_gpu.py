@@ -120,12 +120,14 @@ CUBE_PATHS = [{}, {"cube_kernel": "small"}, {"cube_kernel": "fused"},
               {"cube_kernel": "fused", "cube_rows_per_instr": 2},
               {"cube_kernel": "fused", "cube_rows_per_instr": 1}, {"cube_kernel": "workspace"},
               {"cube_kernel": "generic"}, {"cube_kernel": "fused", "cube_cols_per_lane": 4},
-              {"cube_kernel": "fused", "cube_tile_rows": 32}]
+              {"cube_kernel": "fused", "cube_tile_rows": 32},
+              {"cube_kernel": "fused", "cube_rows_per_instr": 8, "cube_tile_rows": 16},
+              {"cube_kernel": "fused", "cube_rows_per_instr": 4}]
 
 
 @pytest.mark.parametrize("seed", range(64))
 def test_cube_random_vs_oracle(cuda, seed):
-    """Every cube kernel path in turn (seed % 8), the default one included."""
+    """Every cube kernel path in turn (seed % len(CUBE_PATHS)), the default one included."""
     import torch
     from bpc_baseline_amd import ops
     rng = np.random.default_rng(9000 + seed)

@@ -100,7 +100,7 @@ def parse_opts(spec):
     if spec == "default":
         return None
     kw = dict(kv.split("=") for kv in spec.split(","))
-    return _native.make_options(**{k: (v if k == "pairwise_argmin" else int(v))
+    return _native.make_options(**{k: (int(v) if v.lstrip("-").isdigit() else v)
                                    for k, v in kw.items()})
 
 
