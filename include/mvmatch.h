@@ -81,7 +81,7 @@ enum {
     MVM_PAIRWISE_ARGMIN_EAGER            /* best value + index per pair */
 };
 enum {
-    MVM_CUBE_DEFAULT = 0,   /* by the batch's largest view: SMALL <= 44, FUSED above */
+    MVM_CUBE_DEFAULT = 0,   /* by the batch's largest view: SMALL <= 16, FUSED above */
     MVM_CUBE_SMALL,         /* one workgroup per scene (views < 64; FUSED otherwise) */
     MVM_CUBE_FUSED,         /* 16 i x 32 j tiles, pair residuals in the prologue
                                (views <= 256; k-chunked above) */
