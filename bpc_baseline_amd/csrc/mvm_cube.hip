@@ -11,6 +11,7 @@
 // are computed in the prologue (k-chunked above 256), and a workspace form
 // (fp64 pair matrices, then tiles or one row per wave) kept as the exact
 // generic path.
+#include <algorithm>
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -423,6 +424,17 @@ __device__ __forceinline__ uint32_t bm8_key(float v) {
     return v != v ? kBm8NaN : (__float_as_uint(v) | 0x80000000u);
 }
 
+// minimum over the SPLIT lane groups of a split-form wave (lanes l, l + L,
+// l + 2L, ... with L = 64 / SPLIT hold the same k): xor 8 (DPP row_ror:8),
+// xor 16 (swizzle), xor 32 (bpermute)
+template <int SPLIT>
+__device__ __forceinline__ uint32_t min_across_groups(uint32_t v, int lane) {
+    if constexpr (SPLIT >= 8) v = umin(v, dpp_from<0x128>(v));
+    if constexpr (SPLIT >= 4) v = umin(v, (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x1F | (16 << 10)));
+    if constexpr (SPLIT >= 2) v = umin(v, (uint32_t)__builtin_amdgcn_ds_bpermute((lane ^ 32) << 2, (int)v));
+    return v;
+}
+
 // one lane's KPL keys of an 8-row group (k = kb .. kb + KPL - 1, kvalid of
 // them in the view), stored as their upper halves; vec: 8-byte aligned row
 template <int KPL>
@@ -487,13 +499,13 @@ template <int kCubeIB, int kCubeRPW, int SPLIT = 1, int KPL = kColsPerLane, bool
 // kCubeIB: i rows per tile, 16 or (split forms, mvm_options.cube_tile_rows) 32.
 __global__ __launch_bounds__(kThreads, fused_occupancy(kCubeIB, kCubeRPW, SPLIT, KPL, BM8))
 void triplet_fused_kernel(CubeFusedArgs args) {
-    static_assert(!BM8 || (SPLIT == 1 && kCubeRPW == 8), "8-row minima: one row per instruction, 8 per wave");
+    static_assert(!BM8 || kCubeRPW == 8, "8-row minima: 8 rows per wave (one 8-row group)");
     constexpr bool HALF = SPLIT > 1;   // split mapping
     static_assert(SPLIT == 1 || ((kCubeRPW == 8 || kCubeRPW == 12) && (SPLIT == 2 || SPLIT == 4)) ||
                       (kCubeRPW == 8 && SPLIT == 8 && KPL <= 4),
                   "8 or 12 rows in 2 or 4 groups, or 8 rows in 8 groups of 3-4 k per lane");
     static_assert(kCubeRPW % SPLIT == 0, "whole rows per lane group");
-    static_assert(KPL >= 3 && KPL <= 8 && (KPL <= 4 || (SPLIT > 1 && !BM8)),
+    static_assert(KPL >= 3 && KPL <= 8 && (KPL <= 4 || SPLIT > 1),
                   "3 or 4 k per lane; 5-8 in the split forms (views of 65-256 at 2 or 4 rows per "
                   "instruction)");
     constexpr int kLaneRows = kCubeRPW / SPLIT;   // rows a lane computes
@@ -780,7 +792,8 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                     if constexpr (BM8) {
 #pragma unroll
                         for (int q = 0; q < KPL; ++q)
-                            if (act && (whole || q < kvalid)) bmk[q] = umin(bmk[q], bm8_key(v[q]));
+                            if (act && (K2 ? kpos(q) < P : (whole || q < kvalid)))
+                                bmk[q] = umin(bmk[q], bm8_key(v[q]));
                     }
                     Best b{v[0], kb};
 #pragma unroll
@@ -814,9 +827,25 @@ void triplet_fused_kernel(CubeFusedArgs args) {
                 }
             }
             if constexpr (BM8) {
-                if (act_k)
-                    bm8_store<KPL>(args.bmin8 + args.bmin8_offs[s] + ((int64_t)i * ((M + 7) / 8) + j0 / 8) * P,
-                                   kb, kvalid, bmk, (P & 3) == 0 && (args.bmin8_offs[s] & 3) == 0);
+                uint16_t *brow = args.bmin8 + args.bmin8_offs[s] + ((int64_t)i * ((M + 7) / 8) + j0 / 8) * P;
+                if constexpr (HALF) {
+                    // the wave's 8 rows lie on SPLIT lane groups holding the
+                    // same k: the minimum across the groups (lane strides of
+                    // kLPR), then group 0 stores the keys
+#pragma unroll
+                    for (int q = 0; q < KPL; ++q) bmk[q] = min_across_groups<SPLIT>(bmk[q], lane);
+                    if (hl == 0 && act_k) {
+                        if constexpr (K2 == 0) {
+                            bm8_store<KPL>(brow, kb, kvalid, bmk, (P & 3) == 0 && (args.bmin8_offs[s] & 3) == 0);
+                        } else {
+#pragma unroll
+                            for (int q = 0; q < KPL; ++q)
+                                if (kpos(q) < P) brow[kpos(q)] = (uint16_t)(bmk[q] >> 16);
+                        }
+                    }
+                } else if (act_k) {
+                    bm8_store<KPL>(brow, kb, kvalid, bmk, (P & 3) == 0 && (args.bmin8_offs[s] & 3) == 0);
+                }
             }
             if constexpr (HALF) {
                 // each row lies on one group of kLPR lanes: reduce inside the
@@ -1418,24 +1447,67 @@ __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs a
 }
 
 // CubeFusedArgs::bmin8 read back from a finished cube, for the kernel paths
-// that do not emit the 8-row minima themselves: one workgroup per (scene, i).
+// that do not emit the 8-row minima themselves: one workgroup per (scene,
+// block of `ir` rows i), ir chosen so a workgroup has >= ~1,024 items; its
+// threads take the (i, 8-row group, k) items in turn -- four k per item with
+// 16-byte loads where the rows allow, the group's 8 rows loaded together (the
+// round-4 form walked k alone for one i, with 8 dependent loads)
 __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t *cam_offs,
                                                                    const int64_t *cube_offs,
                                                                    const float *cube, uint16_t *bmin8,
-                                                                   const int64_t *bmin8_offs, int max_n) {
-    const int s = (int)(blockIdx.x / (unsigned)max_n), i = (int)(blockIdx.x % (unsigned)max_n);
+                                                                   const int64_t *bmin8_offs, int i_blocks,
+                                                                   int ir) {
+    const int s = (int)(blockIdx.x / (unsigned)i_blocks);
+    const int i0 = (int)(blockIdx.x % (unsigned)i_blocks) * ir;
     const int64_t *co = cam_offs + 3 * (int64_t)s;
     const int N = (int)(co[1] - co[0]), M = (int)(co[2] - co[1]), P = (int)(co[3] - co[2]);
-    if (i >= N || M == 0 || P == 0) return;
+    if (i0 >= N || M == 0 || P == 0) return;
+    const int ni = min(ir, N - i0);
     const int g8 = (M + 7) / 8;
-    const float *base = cube + cube_offs[s] + (int64_t)i * M * P;
-    uint16_t *out = bmin8 + bmin8_offs[s] + (int64_t)i * g8 * P;
-    for (int jg = 0; jg < g8; ++jg) {
-        for (int k = threadIdx.x; k < P; k += kThreads) {
-            uint32_t m = 0xFFFFFFFFu;
-            for (int j = 8 * jg; j < min(8 * jg + 8, M); ++j) m = umin(m, bm8_key(base[(int64_t)j * P + k]));
-            out[(int64_t)jg * P + k] = (uint16_t)(m >> 16);
+    const int64_t cb = cube_offs[s] + (int64_t)i0 * M * P, ob = bmin8_offs[s] + (int64_t)i0 * g8 * P;
+    const float *base = cube + cb;                 // row i0's (j, k) block; row i0 + ii at + ii M P
+    uint16_t *out = bmin8 + ob;                    // ... at + ii g8 P
+    if ((P & 3) == 0 && (cb & 3) == 0 && (ob & 3) == 0) {
+        const int P4 = P / 4, per_i = g8 * P4, items = ni * per_i;
+        for (int x = threadIdx.x; x < items; x += kThreads) {
+            const int ii = x / per_i, y = x - ii * per_i, jg = y / P4, k = 4 * (y - jg * P4);
+            const float *bi = base + (int64_t)ii * M * P;
+            f32x4 v[8];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                const int j = 8 * jg + r;
+                v[r] = j < M ? *reinterpret_cast<const f32x4 *>(bi + (int64_t)j * P + k)
+                             : f32x4{INFINITY, INFINITY, INFINITY, INFINITY};
+            }
+            uint32_t m[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                if (8 * jg + r >= M) continue;
+                m[0] = umin(m[0], bm8_key(v[r].x));
+                m[1] = umin(m[1], bm8_key(v[r].y));
+                m[2] = umin(m[2], bm8_key(v[r].z));
+                m[3] = umin(m[3], bm8_key(v[r].w));
+            }
+            *reinterpret_cast<uint2 *>(out + (int64_t)ii * g8 * P + (int64_t)jg * P + k) =
+                make_uint2((m[0] >> 16) | (m[1] & 0xFFFF0000u), (m[2] >> 16) | (m[3] & 0xFFFF0000u));
         }
+        return;
+    }
+    const int per_i = g8 * P, items = ni * per_i;
+    for (int x = threadIdx.x; x < items; x += kThreads) {
+        const int ii = x / per_i, y = x - ii * per_i, jg = y / P, k = y - jg * P;
+        const float *bi = base + (int64_t)ii * M * P;
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int j = 8 * jg + r;
+            v[r] = j < M ? bi[(int64_t)j * P + k] : INFINITY;
+        }
+        uint32_t m = 0xFFFFFFFFu;
+#pragma unroll
+        for (int r = 0; r < 8; ++r)
+            if (8 * jg + r < M) m = umin(m, bm8_key(v[r]));
+        out[(int64_t)ii * g8 * P + (int64_t)jg * P + k] = (uint16_t)(m >> 16);
     }
 }
 
@@ -1496,10 +1568,14 @@ int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs
                          cube_dev, argmin_dev, minval_dev, bmin8_dev, bmin8_offs_dev, workspace_dev,
                          workspace_bytes, opts, s, emitted);
     if (st || !bmin8_dev || emitted || n_scenes == 0 || max_n == 0) return st;
-    const int64_t blocks = (int64_t)n_scenes * max_n;
+    // rows i per workgroup: >= ~1,024 (i, group, 4 k) items at the largest view
+    const int64_t per_i = (int64_t)((max_n + 7) / 8) * ((max_n + 3) / 4);
+    const int ir = (int)std::min<int64_t>(max_n, std::max<int64_t>(1, (1024 + per_i - 1) / per_i));
+    const int i_blocks = (max_n + ir - 1) / ir;
+    const int64_t blocks = (int64_t)n_scenes * i_blocks;
     if ((st = grid_check(blocks))) return st;
     bmin8_from_cube_kernel<<<dim3((unsigned)blocks), dim3(kThreads), 0, s>>>(
-        cam_offs_dev, cube_offs_dev, cube_dev, bmin8_dev, bmin8_offs_dev, max_n);
+        cam_offs_dev, cube_offs_dev, cube_dev, bmin8_dev, bmin8_offs_dev, i_blocks, ir);
     return mvm_check_launch("bmin8_from_cube_kernel");
 }
 
@@ -1518,30 +1594,38 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
 
 namespace {
 
-// the fused kernel at two / four rows per instruction, tiles of IB i rows
-template <int IB>
+// the fused kernel at two / four / eight rows per instruction, tiles of IB i
+// rows; BM8: it also writes the 8-row minima (not the 48-j tiles' 12-row waves)
+template <int IB, bool BM8 = false>
 void launch_split(int split, int kpl, bool j48, dim3 grid, dim3 block, hipStream_t s, const CubeFusedArgs &c) {
     if (split == 8) {   // views of <= 32: eight rows per instruction
-        if (kpl == 3) triplet_fused_kernel<IB, 8, 8, 3><<<grid, block, 0, s>>>(c);
-        else triplet_fused_kernel<IB, 8, 8, 4><<<grid, block, 0, s>>>(c);
+        if (kpl == 3) triplet_fused_kernel<IB, 8, 8, 3, BM8><<<grid, block, 0, s>>>(c);
+        else triplet_fused_kernel<IB, 8, 8, 4, BM8><<<grid, block, 0, s>>>(c);
+        return;
+    }
+    if constexpr (BM8 && IB == 32) {   // not launched (the host's bm8 rule): not instantiated
+        return;
     } else if (split == 4) {
-        switch (j48 ? 0 : kpl) {
-        case 0: triplet_fused_kernel<IB, 12, 4, 3><<<grid, block, 0, s>>>(c); break;
-        case 3: triplet_fused_kernel<IB, 8, 4, 3><<<grid, block, 0, s>>>(c); break;
-        case 4: triplet_fused_kernel<IB, 8, 4><<<grid, block, 0, s>>>(c); break;
-        case 5: triplet_fused_kernel<IB, 8, 4, 5><<<grid, block, 0, s>>>(c); break;
-        case 6: triplet_fused_kernel<IB, 8, 4, 6><<<grid, block, 0, s>>>(c); break;
-        case 7: triplet_fused_kernel<IB, 8, 4, 7><<<grid, block, 0, s>>>(c); break;
-        default: triplet_fused_kernel<IB, 8, 4, 8><<<grid, block, 0, s>>>(c); break;
+        if (j48 && !BM8) {
+            triplet_fused_kernel<IB, 12, 4, 3><<<grid, block, 0, s>>>(c);
+            return;
+        }
+        switch (kpl) {
+        case 3: triplet_fused_kernel<IB, 8, 4, 3, BM8><<<grid, block, 0, s>>>(c); break;
+        case 4: triplet_fused_kernel<IB, 8, 4, 4, BM8><<<grid, block, 0, s>>>(c); break;
+        case 5: triplet_fused_kernel<IB, 8, 4, 5, BM8><<<grid, block, 0, s>>>(c); break;
+        case 6: triplet_fused_kernel<IB, 8, 4, 6, BM8><<<grid, block, 0, s>>>(c); break;
+        case 7: triplet_fused_kernel<IB, 8, 4, 7, BM8><<<grid, block, 0, s>>>(c); break;
+        default: triplet_fused_kernel<IB, 8, 4, 8, BM8><<<grid, block, 0, s>>>(c); break;
         }
     } else {
         switch (kpl) {
-        case 3: triplet_fused_kernel<IB, 8, 2, 3><<<grid, block, 0, s>>>(c); break;
-        case 4: triplet_fused_kernel<IB, 8, 2><<<grid, block, 0, s>>>(c); break;
-        case 5: triplet_fused_kernel<IB, 8, 2, 5><<<grid, block, 0, s>>>(c); break;
-        case 6: triplet_fused_kernel<IB, 8, 2, 6><<<grid, block, 0, s>>>(c); break;
-        case 7: triplet_fused_kernel<IB, 8, 2, 7><<<grid, block, 0, s>>>(c); break;
-        default: triplet_fused_kernel<IB, 8, 2, 8><<<grid, block, 0, s>>>(c); break;
+        case 3: triplet_fused_kernel<IB, 8, 2, 3, BM8><<<grid, block, 0, s>>>(c); break;
+        case 4: triplet_fused_kernel<IB, 8, 2, 4, BM8><<<grid, block, 0, s>>>(c); break;
+        case 5: triplet_fused_kernel<IB, 8, 2, 5, BM8><<<grid, block, 0, s>>>(c); break;
+        case 6: triplet_fused_kernel<IB, 8, 2, 6, BM8><<<grid, block, 0, s>>>(c); break;
+        case 7: triplet_fused_kernel<IB, 8, 2, 7, BM8><<<grid, block, 0, s>>>(c); break;
+        default: triplet_fused_kernel<IB, 8, 2, 8, BM8><<<grid, block, 0, s>>>(c); break;
         }
     }
 }
@@ -1661,7 +1745,9 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
         // views of 33-48 at four rows per instruction and 3 k per lane: tiles
         // of 48 j (12 rows per wave), so a view of 48 fills one tile instead of
         // leaving half of a second 32-wide tile empty
-        const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8;
+        // (not when the 8-row minima are wanted: the 8-row waves write them,
+        // the 12-row ones would leave them to a pass over the cube)
+        const bool j48 = split == 4 && kpl == 3 && max_n > kWaves * 8 && !bmin8_dev;
         // i rows per tile: 32 on request in the split forms (ABI 6), and by
         // default at eight rows per instruction (views of <= 32: a tile of
         // 16 i rows of such a view is mostly prologue; 24^3 0.663 -> 0.571,
@@ -1681,8 +1767,19 @@ int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double
             return mvm_check_launch("triplet_fused_chunked_kernel");
         }
         if (split > 1) {
-            if (tile_rows == 32) launch_split<32>(split, kpl, j48, grid, block, s, c);
-            else launch_split<16>(split, kpl, j48, grid, block, s, c);
+            // the 8-row minima from the same kernel, but for the 48-j tiles
+            // (12 rows per wave); tiles of 32 i rows at eight rows per
+            // instruction, 16 otherwise (the shapes the defaults take)
+            const bool bm8 = bmin8_dev && !j48 && tile_rows == (split == 8 ? 32 : 16);
+            if (bm8) {
+                if (tile_rows == 32) launch_split<32, true>(split, kpl, j48, grid, block, s, c);
+                else launch_split<16, true>(split, kpl, j48, grid, block, s, c);
+                emitted = true;
+            } else if (tile_rows == 32) {
+                launch_split<32>(split, kpl, j48, grid, block, s, c);
+            } else {
+                launch_split<16>(split, kpl, j48, grid, block, s, c);
+            }
         } else if (bmin8_dev) {                  // the 8-row minima from the same kernel
             if (kpl == 3) triplet_fused_kernel<16, 8, 1, 3, true><<<grid, block, 0, s>>>(c);
             else triplet_fused_kernel<16, 8, 1, kColsPerLane, true><<<grid, block, 0, s>>>(c);

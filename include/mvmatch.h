@@ -253,10 +253,11 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
  * bmin8_dev + bmin8_offs_dev[s] holds, per k, the upper 16 bits of the
  * order-preserving key (float bits | 0x80000000) of min over j in [8g, 8g+8)
  * of cube[i][j][k] -- a lower bound of that minimum to 1/128 -- or 0 when any
- * of the eight is NaN.  The fused kernel of views of 129-256 detections
- * writes them itself; every other path reads them back from the cube
- * (cube_dev required).  Offsets that are multiples of 4 keys let the kernel
- * store 8 bytes per lane.
+ * of the eight is NaN.  The fused kernel (views of 17-256 detections, its
+ * default shapes; with them requested, views of 33-48 take 32-j instead of
+ * 48-j tiles) writes them itself; every other path reads them back from the
+ * cube (cube_dev required).  Offsets that are multiples of 4 keys let the
+ * kernel store 8 bytes per lane.
  */
 int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs_dev,
                                   const double *F_dev, int32_t n_scenes, int32_t max_n,

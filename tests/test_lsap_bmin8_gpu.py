@@ -39,23 +39,33 @@ def _run(cuda, counts, seed, options=None, nan_scene=None, nan_view=2):
     return plan, cube, bm8
 
 
-# batches by largest view (it picks the cube kernel): 129-256 the fused kernel
-# writes the minima itself (3 and 4 k per lane), <= 128 and > 256 they are
-# read back from the cube
+# batches by largest view (it picks the cube kernel): the fused kernel writes
+# the minima itself at one, two, four and eight rows per instruction (3 or 4 k
+# per lane, or 5-8 in two panels); the 48-j tiles (views of 33-48), forced
+# 32-row tiles at two or four rows per instruction, the small kernel (<= 16),
+# the k-chunked kernel (> 256) and the workspace / generic paths read them back
+# from the cube
 BATCHES = {
     "fused": [(20, 256, 256), (7, 250, 193), (9, 131, 200), (5, 130, 64), (3, 45, 40), (4, 0, 9),
               (6, 33, 0), (11, 8, 1)],
     "fused_kpl3": [(9, 150, 190), (4, 177, 131), (6, 131, 1)],
     "small_views": [(12, 100, 128), (5, 64, 70), (3, 45, 40), (2, 0, 5)],
     "chunked": [(2, 300, 20), (3, 260, 257), (2, 50, 300)],
+    "rows2_panels": [(6, 100, 150), (4, 130, 129), (3, 9, 140), (2, 1, 1)],
+    "rows4": [(9, 64, 60), (5, 33, 17), (3, 40, 64), (4, 7, 3)],
+    "rows4_panels": [(6, 100, 100), (4, 90, 110), (2, 3, 97)],
+    "rows8": [(7, 32, 30), (4, 17, 25), (3, 9, 5), (2, 31, 1)],
+    "j48": [(5, 48, 40), (3, 40, 33)],
+    "tiny": [(3, 16, 16), (4, 5, 12)],
 }
 
 
 @pytest.mark.parametrize("batch", sorted(BATCHES))
-@pytest.mark.parametrize("path", ["default", "workspace", "generic", "kpl4"])
+@pytest.mark.parametrize("path", ["default", "workspace", "generic", "kpl4", "rows4", "tile32"])
 def test_bmin8_equals_numpy(cuda, path, batch):
     opts = {"default": None, "workspace": {"cube_kernel": "workspace"},
-            "generic": {"cube_kernel": "generic"}, "kpl4": {"cube_cols_per_lane": 4}}[path]
+            "generic": {"cube_kernel": "generic"}, "kpl4": {"cube_cols_per_lane": 4},
+            "rows4": {"cube_rows_per_instr": 4}, "tile32": {"cube_tile_rows": 32}}[path]
     counts = BATCHES[batch]
     plan, cube, bm8 = _run(cuda, counts, 3, opts)
     c = cube.cpu().numpy()
@@ -76,6 +86,8 @@ def test_bmin8_equals_numpy(cuda, path, batch):
     [(64, 64, 64), (40, 250, 130), (30, 200, 256), (20, 256, 256), (9, 131, 200), (17, 99, 70),
      (3, 2, 5), (5, 0, 3)],
     [(16, 300, 40), (40, 120, 64), (2, 1000, 7)],
+    [(64, 64, 64), (80, 100, 100), (60, 90, 64)],
+    [(128, 32, 30), (200, 30, 32), (7, 3, 2)],
 ])
 @pytest.mark.parametrize("sparse_from", [0, 1025])
 def test_assignment_from_bmin8_equals_scipy(cuda, sparse_from, counts):
