@@ -286,7 +286,7 @@ __device__ __forceinline__ uint32_t sp_b8_upper(uint32_t h) {
 }
 
 __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a, int32_t n) {
-    constexpr int kKeys = 8192;                            // 32 KiB of LDS keys per pass
+    constexpr int kKeys = 8448;                            // 33 KiB of LDS keys per pass
     constexpr int kTiles = kSpMaxBlocks / 64;
     __shared__ uint32_t s_key[kKeys];
     const int p = (int)(blockIdx.x / kTiles), w = (int)(blockIdx.x % kTiles);
@@ -305,17 +305,18 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
     unsigned char *ws = a.ws + a.ws_offs[p];
     uint32_t *bm = reinterpret_cast<uint32_t *>(ws + y.bm);
     const uint16_t *B8 = a.bmin8 + a.bmin8_offs[p];
+    // LDS keys [column][block], rows of bp + 1 words (the per-(key, block)
+    // stores below walk the keys: stride 1 word mod 32 banks)
     int bp = 64;
-    while (bp > 1 && S * bp > kKeys) bp >>= 1;
+    while (bp > 1 && S * (bp + 1) > kKeys) bp >>= 1;
+    const int RB = bp + 1;
     const int t = threadIdx.x;
     const int G = S / 8;                                   // threads per group row (8 keys each)
     const bool fast = S % 8 == 0 && kSpNT % G == 0 && ((reinterpret_cast<uintptr_t>(B8)) & 15) == 0;
     auto invalid = [](uint32_t h) { return h < 0x8000u; };   // NaN (0); a cube holds no -inf
     int bad = 0;
     for (int pb0 = b0; pb0 < b1; pb0 += bp) {
-        const int pb1 = min(pb0 + bp, b1), nrow = 4 * (pb1 - pb0);   // (block, u) rows
-        for (int x = t; x < S * bp; x += kSpNT) s_key[x] = 0xFFFFu;
-        __syncthreads();
+        const int pb1 = min(pb0 + bp, b1);              // every (key, block < pb1 - pb0) is written below
         // local row x -> its 8-row group, or -1 past the segment's end
         auto group = [&](int x) {
             const int b = pb0 + (x >> 2), u = x & 3;
@@ -360,25 +361,34 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
                     }
 #pragma unroll
                     for (int d = 0; d < 4; ++d) {
-                        s_key[(8 * g8 + 2 * d) * bp + lb] = m[d] & 0xFFFFu;
-                        s_key[(8 * g8 + 2 * d + 1) * bp + lb] = m[d] >> 16;
+                        s_key[(8 * g8 + 2 * d) * RB + lb] = m[d] & 0xFFFFu;
+                        s_key[(8 * g8 + 2 * d + 1) * RB + lb] = m[d] >> 16;
                     }
                 }
             }
         } else {
-            for (int e = t; e < nrow * S; e += kSpNT) {
-                const int x = e / S, sc = e - x * S, r = group(x);
-                if (r < 0) continue;
-                const uint32_t v = B8[(int64_t)r * S + sc];
-                bad |= invalid(v);
-                atomicMin(&s_key[sc * bp + (x >> 2)], v);
+            // any short side: one thread per (key, block), the block's (up
+            // to) four 8-row groups loaded together, consecutive threads on
+            // consecutive keys (the round-4 form: one LDS atomic per key read)
+            const int nbk = pb1 - pb0;
+            for (int e = t; e < S * nbk; e += kSpNT) {
+                const int lb = e / S, sc = e - lb * S;
+                uint32_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = group(4 * lb + u);
+                    v[u] = r >= 0 ? (uint32_t)B8[(int64_t)r * S + sc] : 0xFFFFu;
+                }
+                const uint32_t m = min(min(v[0], v[1]), min(v[2], v[3]));
+                bad |= invalid(m);
+                s_key[sc * RB + lb] = m;
             }
         }
         __syncthreads();
         const int nbk = pb1 - pb0;
         for (int x = t; x < S * nbk; x += kSpNT) {
             const int sc = x / nbk, bb = x - sc * nbk;
-            bm[(int64_t)sc * nb + pb0 + bb] = sp_b8_upper(s_key[sc * bp + bb]);
+            bm[(int64_t)sc * nb + pb0 + bb] = sp_b8_upper(s_key[sc * RB + bb]);
         }
         __syncthreads();
     }
