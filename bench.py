@@ -21,8 +21,10 @@ last piece is exposed, and that last launch is a short one, ~1/4 of the
 others); every residual is stored to HBM.  At every N each
 launch of each timed step of C3 is a hipGraph captured outside the timed
 region and replayed in order, with N > 1 followed by its gather piece, so the
-1 -> N curve compares the same launch path (``--graph steps``, the default
-for C2 on one GPU: one graph for all K steps; ``--graph off``: eager op calls).
+1 -> N curve compares the same launch path (``--graph steps2``, the default
+for C2 on one GPU: one graph for all K steps, even and odd steps on two
+streams; ``--graph steps``: the same on one stream; ``--graph off``: eager op
+calls).
 
 ``python bench.py --gpus N`` (N > 1) run without a launcher starts the N
 ranks itself: torchrun in a child process, this process making no GPU call;
@@ -775,7 +777,7 @@ def main():
     ap.add_argument("--output", choices=["resident", "ring"], default="resident",
                     help="resident (default): one output allocation per launch of the timed "
                          "steps as far as HBM holds them (reused round robin); ring: one")
-    ap.add_argument("--graph", choices=["auto", "launch", "steps", "off"], default="auto",
+    ap.add_argument("--graph", choices=["auto", "launch", "steps", "steps2", "off"], default="auto",
                     help="auto (default): steps for the c2 workload on one GPU (its 0.14 ms "
                          "launches are shorter than the host's per-replay cost), launch "
                          "otherwise; launch: each launch of each timed step is a hipGraph "
@@ -857,9 +859,11 @@ def main():
         # 4 ms launches do.  Events recorded inside a captured graph cannot be
         # timed on ROCm (tools/probes/graph_events.py), so "steps" times the K
         # steps with one event pair.
-        args.graph = "steps" if (args.workload == "c2" and not env.initialised) else "launch"
-    if args.graph == "steps" and env.initialised:
-        raise SystemExit("--graph steps needs a single GPU without a process group "
+        # steps so short that a step's tail and the next one's start matter (C2)
+        # take two streams ("steps2": +6-8% on the C2 line)
+        args.graph = "steps2" if (args.workload == "c2" and not env.initialised) else "launch"
+    if args.graph in ("steps", "steps2") and env.initialised:
+        raise SystemExit("--graph steps/steps2 need a single GPU without a process group "
                          "(the step's gather is a collective)")
     if args.scaling == "strong" and wl["n_scenes"] < world:
         raise SystemExit(f"--scenes {wl['n_scenes']} < {world} ranks: every rank needs at least "
@@ -883,6 +887,9 @@ def main():
     chunks, n_rows = build_chunks(batch, bounds, dev, wl["mode"])
     argmin = torch.empty(n_rows, dtype=torch.int32, device=dev)
     minval = torch.empty(n_rows, dtype=torch.float32, device=dev)
+    # "steps2": the odd steps' association rows (they may run beside an even step)
+    alt_rows = ((torch.empty_like(argmin), torch.empty_like(minval)) if args.graph == "steps2"
+                else None)
     max_units = max(c.size for c in chunks)
     # output slots: one allocation per launch of the timed steps when they fit
     # (a step's residuals all stay resident, and consecutive steps write other
@@ -908,9 +915,10 @@ def main():
     units_local = sum(c.units for c in chunks)
     stream = torch.cuda.current_stream(dev)
 
-    def launch(c: Chunk):
-        am = argmin[c.row_base:c.row_base + c.plan.n_rows]
-        mv = minval[c.row_base:c.row_base + c.plan.n_rows]
+    def launch(c: Chunk, alt: bool = False):
+        am_all, mv_all = alt_rows if alt else (argmin, minval)
+        am = am_all[c.row_base:c.row_base + c.plan.n_rows]
+        mv = mv_all[c.row_base:c.row_base + c.plan.n_rows]
         last_slot[id(c)] = seq[0] % n_slots
         slot_owner[last_slot[id(c)]] = c.idx
         seq[0] += 1
@@ -969,12 +977,26 @@ def main():
             for g in row:
                 g.replay()
                 dispatched[0] += 1
-    elif args.graph == "steps":
+    elif args.graph in ("steps", "steps2"):
+        # steps2: the K steps captured on two streams, even steps on one and
+        # odd steps on the other (each step writes its own output allocation
+        # and, for odd steps, its own association rows), so consecutive steps
+        # are independent graph branches and one step's tail may overlap the
+        # next one's start
         step_graph = torch.cuda.CUDAGraph()
+        two = args.graph == "steps2"
+        alt_stream = torch.cuda.Stream(dev) if two else None
         with torch.cuda.graph(step_graph, **cap_kw):
-            for _ in range(args.steps):
-                for c in chunks:
-                    launch(c)
+            cs = torch.cuda.current_stream(dev)
+            if two:
+                alt_stream.wait_stream(cs)
+            for st in range(args.steps):
+                odd = two and st % 2 == 1
+                with torch.cuda.stream(alt_stream if odd else cs):
+                    for c in chunks:
+                        launch(c, alt=odd)
+            if two:
+                cs.wait_stream(alt_stream)
         step_graph.replay()
         dispatched[0] += args.steps * len(chunks)
     torch.cuda.synchronize(dev)
@@ -1036,6 +1058,10 @@ def main():
         env.barrier()
         elapsed = time.perf_counter() - t_start
     window_timed = dispatched[0] - window_start
+    if alt_rows is not None and (args.steps - 1) % 2 == 1:   # the last step's rows (untimed)
+        argmin.copy_(alt_rows[0])
+        minval.copy_(alt_rows[1])
+        torch.cuda.synchronize(dev)
     elapsed = max_over_ranks(env, elapsed)
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -1265,6 +1291,9 @@ def main():
                    "is issued right after its replay"),
         "steps": ("one hipGraph holding the K steps' launches, captured once outside the timed "
                   "region, replayed once"),
+        "steps2": ("one hipGraph holding the K steps' launches on two streams (even / odd "
+                   "steps; each step its own output allocation, odd steps their own "
+                   "association rows), captured once outside the timed region, replayed once"),
         "off": "eager op calls",
     }[args.graph]
     out = {

@@ -190,7 +190,8 @@ def test_ranks_real_kernel_equal_single_process(tmp_path, world, n_scenes):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("workload,mode", [("c3", "steps"), ("c2cube", "steps"),
-                                           ("c3", "launch"), ("c2cube", "launch")])
+                                           ("c3", "launch"), ("c2cube", "launch"),
+                                           ("c3", "steps2"), ("c3", "steps2-3")])
 def test_bench_graph_replay_single_gpu(tmp_path, workload, mode):
     """bench.py's single-GPU timed steps as hipGraph replays (one graph for the
     K steps, or one per launch): the captured launches of every step run (the
@@ -203,21 +204,26 @@ def test_bench_graph_replay_single_gpu(tmp_path, workload, mode):
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ)
     env.pop("MVM_DIST_FORCE", None)
+    # steps2-3: three steps on two streams (the last one odd-numbered: even),
+    # steps2 with two (the last one on the second stream's association rows)
+    mode, steps = (mode.split("-")[0], int(mode.split("-")[1])) if "-" in mode else (mode, 2)
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", workload,
-                        "--scenes", "24", "--chunk", "8", "--steps", "2", "--warmup", "1",
+                        "--scenes", "24", "--chunk", "8", "--steps", str(steps), "--warmup", "1",
                         "--cpu-seconds", "0", "--graph", mode],
                        env=env, capture_output=True, text=True, timeout=300, cwd=repo)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["parity"].startswith("bit-exact")
+    pr = line["parity_rows"]          # "ok/total bit-exact vs oracle" (a mismatch exits 3)
+    assert pr is None or pr.split("/")[0] == pr.split("/")[1].split()[0]
     assert line["config"]["launch_mode"] == mode
-    assert line["config"]["launch"].startswith("one hipGraph holding the K steps" if mode == "steps"
+    assert line["config"]["launch"].startswith("one hipGraph holding the K steps" if mode.startswith("steps")
                                                else "one hipGraph per launch")
     assert line["config"]["launches_per_step"] == 3
     assert line["roofline"]["avg_launch_ms"] > 0
     w = line["roofline"]["dispatch_window"]
-    # warmup step (3) + the untimed first replay (2 steps x 3) | 2 x 3 timed | PCIe leg (3)
-    assert (w["before"], w["timed"], w["after"]) == (3 + 6, 6, 3)
+    # warmup step (3) + the untimed first replay (K steps x 3) | K x 3 timed | PCIe leg (3)
+    assert (w["before"], w["timed"], w["after"]) == (3 + 3 * steps, 3 * steps, 3)
 
 
 def _bench_env():
