@@ -11,6 +11,8 @@ every one is compared with the oracle bit for bit (float32 values as bit
 patterns, indices exactly).  Found on its first run: the tiled cube kernels
 left the association rows of a scene with an empty third view unwritten.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -20,8 +22,11 @@ pytestmark = pytest.mark.gpu
 
 EDGE_COUNTS = [0, 1, 2, 3, 4, 5, 31, 32, 33, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512,
                513, 1000, 1023, 1024, 1025, 1100]
-CUBE_COUNTS = [0, 1, 2, 5, 16, 31, 32, 33, 44, 45, 47, 48, 49, 63, 64, 65, 95, 96, 97, 100, 127,
-               128, 129, 191, 192, 193, 200, 256, 257, 300]
+CUBE_COUNTS = [0, 1, 2, 5, 16, 17, 24, 25, 31, 32, 33, 44, 45, 47, 48, 49, 63, 64, 65, 80, 81, 95,
+               96, 97, 100, 112, 113, 127, 128, 129, 160, 161, 191, 192, 193, 200, 224, 225, 256, 257,
+               300]
+# seeds per sweep (MVM_RANDOM_SEEDS=600 for a long one-off run)
+N_SEEDS = int(os.environ.get("MVM_RANDOM_SEEDS", "64"))
 
 
 def _bits(a):
@@ -72,7 +77,7 @@ def _batch(rng, S, C, counts_of, nonfinite=False):
     return np.ascontiguousarray(pts), cam_offs, np.ascontiguousarray(np.concatenate(Fs)), pairs
 
 
-@pytest.mark.parametrize("seed", range(64))
+@pytest.mark.parametrize("seed", range(N_SEEDS))
 def test_pairwise_random_vs_oracle(cuda, seed):
     import torch
     from bpc_baseline_amd import ops
@@ -125,7 +130,7 @@ CUBE_PATHS = [{}, {"cube_kernel": "small"}, {"cube_kernel": "fused"},
               {"cube_kernel": "fused", "cube_rows_per_instr": 4}]
 
 
-@pytest.mark.parametrize("seed", range(64))
+@pytest.mark.parametrize("seed", range(N_SEEDS))
 def test_cube_random_vs_oracle(cuda, seed):
     """Every cube kernel path in turn (seed % len(CUBE_PATHS)), the default one included."""
     import torch
