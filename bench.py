@@ -908,6 +908,17 @@ def main():
                 raise
             break
     n_slots = len(out_slots)
+    if args.graph == "steps2":
+        # concurrent (even / odd) steps must not share an allocation: with a
+        # multiple of 2 x launches-per-step slots, even steps take one half of
+        # the residues and odd steps the other; too few slots: one stream
+        L2 = 2 * len(chunks)
+        if n_slots >= L2:
+            n_slots = n_slots // L2 * L2
+            del out_slots[n_slots:]
+        else:
+            log(f"--graph steps2 needs >= {L2} output allocations ({n_slots}): one stream")
+            args.graph, alt_rows = "steps", None
     seq = [0]             # launches issued (or captured) so far: the next slot
     last_slot = {}        # chunk -> the slot its latest launch wrote
     slot_owner = {}       # slot -> index of the chunk whose output it holds
