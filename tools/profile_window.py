@@ -39,7 +39,8 @@ def kernel_durations(trace, name_part):
                 rows.append((int(r["Dispatch_Id"]), int(r["Start_Timestamp"]),
                              int(r["End_Timestamp"]), r["Kernel_Name"]))
     rows.sort()
-    return [(e - s) * 1e-6 for _, s, e, _ in rows], sorted({r[3] for r in rows})
+    return ([(e - s) * 1e-6 for _, s, e, _ in rows], sorted({r[3] for r in rows}),
+            [(s, e) for _, s, e, _ in rows])
 
 
 def stats(ms):
@@ -61,7 +62,7 @@ def main():
     rf = line["roofline"]
     w = rf["dispatch_window"]
     name = w["kernel"] + "<"
-    durs, names = kernel_durations(args.trace_csv, name)
+    durs, names, spans = kernel_durations(args.trace_csv, name)
     before, timed, after = w["before"], w["timed"], w["after"]
     if len(durs) != before + timed + after:
         sys.exit(f"trace has {len(durs)} {name} dispatches, the bench line expects "
@@ -72,6 +73,13 @@ def main():
     st = stats(t_ms)
     bpl = rf["bytes_per_launch"]
     frac_trace = bpl / (st["avg_ms"] * 1e-3) / 1e9 / rf["peak"]
+    # the timed launches' span (first start to last end) per launch: the
+    # period the trace shows when launches overlap (--graph steps2: even and
+    # odd steps on two streams), where a launch's own duration includes the
+    # time it shared the GPU with its neighbour
+    ts = spans[before:before + timed]
+    span_ms = (max(e for _, e in ts) - min(s for s, _ in ts)) * 1e-6 / timed
+    frac_span = bpl / (span_ms * 1e-3) / 1e9 / rf["peak"]
     per_slot = []
     for s in range(S):
         first = [durs[n] for n in range(warm) if n % S == s][:1]
@@ -95,6 +103,9 @@ def main():
         "timed": st,
         "timed_frac_of_peak_from_trace": frac_trace,
         "trace_vs_bench_frac": frac_trace / rf["frac"],
+        "timed_span_per_launch_ms": span_ms,
+        "span_frac_of_peak_from_trace": frac_span,
+        "span_vs_bench_frac": frac_span / rf["frac"],
         "timed_sum_per_step_ms": st["avg_ms"] * L,
         "before": stats(durs[:before]),
         "after": stats(durs[before + timed:]),
@@ -107,7 +118,8 @@ def main():
     print(f"timed {st['launches']} launches: avg {st['avg_ms']:.4f} ms (min {st['min_ms']:.4f}, "
           f"max {st['max_ms']:.4f}); frac from trace {frac_trace:.4f} vs bench {rf['frac']:.4f} "
           f"(ratio {frac_trace / rf['frac']:.4f}); {L} x avg = {st['avg_ms'] * L:.3f} ms vs "
-          f"ms_per_step {line['ms_per_step']:.3f}")
+          f"ms_per_step {line['ms_per_step']:.3f}; span {span_ms:.4f} ms per launch, frac "
+          f"{frac_span:.4f} (ratio {frac_span / rf['frac']:.4f})")
     for p in per_slot:
         print("  slot %2d  first %s  retouch %s  replay %s  timed %s (%s..%s, n=%d)" % (
             p["slot"], *("%.3f" % v if v is not None else "  -  " for v in (
