@@ -16,6 +16,15 @@
 #                                             counters, one --pmc pass each
 #   bash tools/gpu.sh match [bench args]      the c2match line (cube + assignment + select)
 #                                             and its kernel trace
+#   bash tools/gpu.sh cubeab LIBS "SIZES" [OPTS]  cube builds / option sets on the same output
+#                                             buffers (tools/ab_same_buffers.py), ~CUBE_BYTES
+#                                             (8e9) per launch; a size is N or N,M,P
+#   bash tools/gpu.sh cubecheck LIBS "SIZES" [OPTS]  the cube parity suites, then cubeab
+#   bash tools/gpu.sh lsapcheck               the assignment suites, the c2match line twice
+#                                             and its kernel trace
+#   bash tools/gpu.sh bm8ab                   the 8-row-minima and assignment suites, then
+#                                             the assignment's block-minima source by view
+#                                             size (tools/ab_bmin8_input.py)
 #   AB_LIBS="a.so b.so" bash tools/gpu.sh ab CMD...
 #                                             in-tree library builds (MVM_LIB_PATH) timed by
 #                                             CMD in alternating processes, AB_ROUNDS rounds
@@ -106,6 +115,37 @@ match)
     -o run -- python -u bench.py --workload c2match --cpu-seconds 0 "$@" > "$O/trace_c2match.json" \
     2> "$O/trace_c2match.err"
   rc=$?; echo "match trace rc=$rc (run it last: nothing after a crashed process)"; exit $rc ;;
+cubeab)
+  for D in $2; do
+    SC=$(python -c "import math,os;d=[int(x) for x in '$D'.split(',')];d=d*3 if len(d)==1 else d;print(max(1,int(float(os.environ.get('CUBE_BYTES','8e9'))/(4*math.prod(d)))))")
+    timeout -k 10 300 python -u tools/ab_same_buffers.py --libs "$1" --workload cube --dets "$D" \
+      --scenes "$SC" --buffers 3 --rounds 2 --opts "${3:-default}" > "$O/ab_$D.log" 2>&1 \
+      || fail "cubeab $D" "$O/ab_$D.log"
+    echo "$D ($SC scenes): $(tail -1 "$O/ab_$D.log")"
+  done ;;
+cubecheck)
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_random_gpu.py \
+    tests/test_lsap_bmin8_gpu.py -x -q -k "cube or bmin8" --timeout 240 --timeout-method thread \
+    > "$O/pytest_cube.log" 2>&1 || fail "cube suites" "$O/pytest_cube.log"
+  tail -1 "$O/pytest_cube.log"
+  bash "$0" cubeab "$@" ;;
+lsapcheck)
+  timeout -k 10 600 python -u -m pytest tests/test_lsap_bmin8_gpu.py tests/test_lsap_gpu.py \
+    tests/test_batch_match_gpu.py -x -q --timeout 240 --timeout-method thread \
+    > "$O/pytest_lsap.log" 2>&1 || fail "assignment suites" "$O/pytest_lsap.log"
+  tail -1 "$O/pytest_lsap.log"
+  bash "$0" match ;;
+bm8ab)
+  timeout -k 10 600 python -u -m pytest tests/test_lsap_bmin8_gpu.py tests/test_lsap_gpu.py \
+    tests/test_batch_match_gpu.py -x -q --timeout 240 --timeout-method thread \
+    > "$O/pytest_bm8.log" 2>&1 || fail "bmin8 suites" "$O/pytest_bm8.log"
+  tail -1 "$O/pytest_bm8.log"
+  for spec in 1000:64 1000:100 1000:128 300:150 300:256 2000:48; do
+    echo "== ${spec#*:} x ${spec%%:*}"
+    timeout -k 10 200 python tools/ab_bmin8_input.py --scenes "${spec%%:*}" --dets "${spec#*:}" \
+      > "$O/bm8ab_${spec#*:}.log" 2>&1 || fail "bm8ab $spec" "$O/bm8ab_${spec#*:}.log"
+    grep -E "minima|itself" "$O/bm8ab_${spec#*:}.log"
+  done ;;
 ab)
   for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
     for lib in $AB_LIBS; do
