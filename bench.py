@@ -525,21 +525,42 @@ def match_cpu_chain(batch, proj, s: int, threshold: float, nthreads: int = 1):
 
 
 def run_match(args, env, wl, kernel_options):
-    """The ``c2match`` workload: what ``match_objects`` returns, at C2 scale.
+    """``--workload c2match``: match_line() printed as the run's JSON line."""
+    line, ok = match_line(args, env, wl, kernel_options, steps=args.steps, warmup=args.warmup,
+                          cube_mode=args.cube, cpu_seconds=args.cpu_seconds,
+                          n_chunks_req=args.match_chunks, lsap_input=args.lsap_input)
+    if line is None:
+        return
+    print(json.dumps(line), flush=True)
+    if not ok:
+        log("error: c2match parity")
+        raise SystemExit(3)
+
+
+def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free", cpu_seconds=0.0,
+               n_chunks_req=1, lsap_input="bmin8"):
+    """What ``match_objects`` returns, at C2 scale (the ``c2match`` workload).
 
     A step is every scene of this rank through the device chain of
     ``batch_match.match_captures`` with its plans built once (the counts are
-    host knowledge): the compute_cost_matrix cube (mvm_triplet_cost_argmin),
-    scipy's linear_sum_assignment of every flattened (N*M, P) cube
-    (mvm_lsap_solve), then threshold + stable cost sort + DLT
-    (mvm_select_triangulate) -- epipolar_matching.py:83-116 and
-    process_pose.py:182-187.  Units are captures (scenes); HIP events time
-    each stage.  After timing, a few scenes are checked against the CPU chain:
-    the cube bit for bit, the assignment pair for pair, the matches and their
-    order exactly and the triangulated points to 1e-10."""
+    host knowledge).  ``cube_mode="free"`` (the default, what
+    ``match_captures(keep_cube=False)`` runs): the cube's 8-row minima and the
+    scenes' fp64 pair residuals (mvm_triplet_minima), the scipy-identical
+    assignment of every flattened (N*M, P) cube recomputing the entries it reads
+    from them (mvm_lsap_solve_resid), then threshold + stable cost sort + DLT
+    (mvm_select_triangulate_resid).  ``"keep"``: the compute_cost_matrix cube
+    (mvm_triplet_cost_argmin + its 8-row minima), the assignment reading it
+    (mvm_lsap_solve_ex3), select + DLT from it.  epipolar_matching.py:83-116 and
+    process_pose.py:182-187.  Units are captures (scenes); HIP events time each
+    stage.  After timing, four scenes are checked against the CPU chain: the
+    cube (keep) or the 8-row minima and the pair residuals (free) bit for bit,
+    the assignment pair for pair, the matches and their order exactly, their
+    costs bit for bit and the triangulated points to 1e-10.
+    -> (line dict on rank 0 / None elsewhere, parity ok)."""
     from bpc_baseline_amd.distributed import shard_range
     from bpc_baseline_amd.inference.utils.camera_utils import projection_matrices
     dev, world = env.device, env.world
+    free = cube_mode == "free"
     if args.scaling == "weak":
         first, n_local = env.rank * wl["n_scenes"], wl["n_scenes"]
     else:
@@ -556,7 +577,7 @@ def run_match(args, env, wl, kernel_options):
     # assignment overlaps the HBM-bound cube of the next chunk (the cube of a
     # chunk waits for the previous step's use of its buffers).  --match-chunks 1
     # is the serial chain.
-    n_chunks = max(1, min(args.match_chunks, n_local))
+    n_chunks = max(1, min(n_chunks_req, n_local))
     bounds = np.linspace(0, n_local, n_chunks + 1).astype(np.int64)
     stream = torch.cuda.current_stream(dev)
     side = torch.cuda.Stream(dev) if n_chunks > 1 else stream
@@ -572,15 +593,22 @@ def run_match(args, env, wl, kernel_options):
         tp = ops.TripletPlan(co_h, b - a, device=dev)
         c3 = tp.counts
         ch["tplan"] = tp
-        ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
-        ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
-        ch["am"] = torch.empty(tp.n_rows, dtype=torch.int32, device=dev)
-        ch["mv"] = torch.empty(tp.n_rows, dtype=torch.float32, device=dev)
-        ch["offs"] = tp.cube_offs[:-1].contiguous()
-        # the cube kernel also writes its 8-row minima, which the assignment
-        # reduces instead of reading the cubes once more (--lsap-input cost: off)
-        ch["bm8"] = (torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
-                     if args.lsap_input == "bmin8" else None)
+        if free:
+            if not ops.cube_free_scenes(c3).all():
+                raise SystemExit("c2match --cube free: a scene outside the candidate-list class")
+            ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
+            ch["cube"] = None
+            ch["bm8"] = torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+        else:
+            ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+            ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
+            ch["am"] = torch.empty(tp.n_rows, dtype=torch.int32, device=dev)
+            ch["mv"] = torch.empty(tp.n_rows, dtype=torch.float32, device=dev)
+            ch["offs"] = tp.cube_offs[:-1].contiguous()
+            # the cube kernel also writes its 8-row minima, which the assignment
+            # reduces instead of reading the cubes once more (--lsap-input cost: off)
+            ch["bm8"] = (torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+                         if lsap_input == "bmin8" else None)
         ch["used"] = None                   # event: the previous step's reads of the buffers
         chunks.append(ch)
 
@@ -592,9 +620,13 @@ def run_match(args, env, wl, kernel_options):
                 stream.wait_event(ch["used"])
             if ev:
                 ev[k][0].record(stream)
-            ops.triplet_cost_argmin(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"],
-                                    out=(ch["cube"], ch["am"], ch["mv"]), options=kernel_options,
-                                    bmin8=ch["bm8"])
+            if free:
+                ops.triplet_minima(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"], bmin8=ch["bm8"],
+                                   options=kernel_options)
+            else:
+                ops.triplet_cost_argmin(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"],
+                                        out=(ch["cube"], ch["am"], ch["mv"]), options=kernel_options,
+                                        bmin8=ch["bm8"])
             e = torch.cuda.Event()
             e.record(stream)
             cube_done.append(e)
@@ -605,15 +637,23 @@ def run_match(args, env, wl, kernel_options):
             with torch.cuda.stream(side):
                 if ev:
                     ev[k][2].record(side)
-                bm8_args = ((ch["bm8"], ch["tplan"].bmin8_offs, ch["tplan"].segs)
-                            if ch["bm8"] is not None else None)
-                r, c, st = ops.linear_sum_assignment_batched(ch["cube"], ch["offs"], ch["lplan"],
-                                                             options=kernel_options, bmin8=bm8_args)
+                if free:
+                    r, c, st = ops.linear_sum_assignment_resid(ch["lplan"], ch["tplan"], ch["bm8"],
+                                                               options=kernel_options)
+                else:
+                    bm8_args = ((ch["bm8"], ch["tplan"].bmin8_offs, ch["tplan"].segs)
+                                if ch["bm8"] is not None else None)
+                    r, c, st = ops.linear_sum_assignment_batched(ch["cube"], ch["offs"], ch["lplan"],
+                                                                 options=kernel_options, bmin8=bm8_args)
                 if ev:
                     ev[k][3].record(side)
-                res = ops.select_triangulate(ch["cube"], ch["tplan"].cube_offs, ch["cam_offs"],
-                                             ch["lplan"].out_offs, r, c, ch["pts"], ch["proj"],
-                                             threshold)
+                if free:
+                    res = ops.select_triangulate_resid(ch["tplan"], ch["cam_offs"], ch["lplan"].out_offs,
+                                                       r, c, ch["pts"], ch["proj"], threshold)
+                else:
+                    res = ops.select_triangulate(ch["cube"], ch["tplan"].cube_offs, ch["cam_offs"],
+                                                 ch["lplan"].out_offs, r, c, ch["pts"], ch["proj"],
+                                                 threshold)
                 if ev:
                     ev[k][4].record(side)
                 u = torch.cuda.Event()
@@ -623,16 +663,16 @@ def run_match(args, env, wl, kernel_options):
         stream.wait_stream(side)
         return outs
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     evs = [[[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in chunks]
-           for _ in range(args.steps)]
+           for _ in range(steps)]
     env.barrier()
     torch.cuda.synchronize(dev)
     with ClockSampler(dev) as clocks:
         t_start = time.perf_counter()
-        for s_ in range(args.steps):
+        for s_ in range(steps):
             outs = step(evs[s_])
         torch.cuda.synchronize(dev)
         env.barrier()
@@ -647,12 +687,12 @@ def run_match(args, env, wl, kernel_options):
     status = np.concatenate([o[2].cpu().numpy() for o in outs])
     count_h = np.concatenate([o[6].cpu().numpy() for o in outs])
     n_matches = sum_over_ranks(env, int(count_h.sum()))
-    tplan_counts = np.concatenate([ch["tplan"].counts for ch in chunks])
     n_bmin8 = sum(ch["tplan"].n_bmin8 for ch in chunks)
 
     # ---- parity (untimed): a few scenes against the CPU chain --------------
     parity_ok, detail = bool((status == 0).all()), []
     if env.is_root:
+        from oracle import oracle as O
         picks = sorted({0, n_local // 3, (2 * n_local) // 3, n_local - 1})
         for s in picks:
             k_ch = int(np.searchsorted(bounds, s, side="right")) - 1
@@ -661,9 +701,28 @@ def run_match(args, env, wl, kernel_options):
             r, c, st, match, cost, X, count = out
             rc, rr, rcol, rm, rX = match_cpu_chain(batch, proj, s, threshold,
                                                    nthreads=cpu_threads())
-            o = int(ch["tplan"].cube_offs_host[sl])
-            cube_ok = np.array_equal(ch["cube"][o:o + rc.size].cpu().numpy().view(np.int32),
-                                     rc.view(np.int32))
+            n3 = tuple(int(x) for x in ch["tplan"].counts[sl])
+            tp = ch["tplan"]
+            if free:
+                # the 8-row minima and the pair residuals the assignment read
+                o8 = int(tp.bmin8_offs_host[sl])
+                n8 = n3[0] * ((n3[1] + 7) // 8) * n3[2]
+                keys = ch["bm8"][o8:o8 + n8].cpu().numpy().view(np.uint16)
+                keys_ok = np.array_equal(keys, O.bmin8_keys(rc.reshape(n3)).reshape(-1))
+                co1 = batch.cam_offs[3 * s:3 * s + 4]
+                want_r = O.residuals(batch.pts[int(co1[0]):int(co1[3])], co1 - co1[0],
+                                     batch.F[3 * s:3 * s + 3], 1, tp.max_n)[0]
+                ld = want_r.shape[-1]
+                stride = 3 * tp.max_n * ld
+                got_r = tp.workspace[:tp.workspace_bytes].view(torch.float64)[sl * stride:(sl + 1) * stride]
+                got_r = got_r.cpu().numpy().reshape(3, tp.max_n, ld)
+                resid_ok = all(np.array_equal(got_r[m, :a_, :b_].view(np.int64), want_r[m, :a_, :b_].view(np.int64))
+                               for m, (a_, b_) in enumerate(((n3[0], n3[1]), (n3[2], n3[0]), (n3[2], n3[1]))))
+                cube_ok = keys_ok and resid_ok
+            else:
+                o = int(tp.cube_offs_host[sl])
+                cube_ok = np.array_equal(ch["cube"][o:o + rc.size].cpu().numpy().view(np.int32),
+                                         rc.view(np.int32))
             lo = int(ch["lplan"].out_offs_host[sl])
             nn = rr.size
             lsap_ok = (np.array_equal(r[lo:lo + nn].cpu().numpy(), rr)
@@ -672,35 +731,56 @@ def run_match(args, env, wl, kernel_options):
             m_h = match[lo:lo + k].cpu().numpy()
             got = [tuple(int(v) for v in m_h[w]) for w in range(k)]
             match_ok = got == rm
+            cube3 = rc.reshape(n3)
+            cost_ok = match_ok and np.array_equal(
+                cost[lo:lo + k].cpu().numpy().view(np.int32),
+                np.array([cube3[t] for t in rm], np.float32).view(np.int32))
             x_ok = match_ok and (k == 0 or np.allclose(X[lo:lo + k].cpu().numpy(), rX, rtol=1e-10,
                                                        atol=1e-9))
-            parity_ok &= bool(cube_ok and lsap_ok and match_ok and x_ok)
-            detail.append({"scene": first + s, "cube_bit_exact": bool(cube_ok),
-                           "assignment_equal": bool(lsap_ok), "matches": k,
-                           "matches_equal_in_order": bool(match_ok), "X_within_1e-10": bool(x_ok)})
+            parity_ok &= bool(cube_ok and lsap_ok and match_ok and cost_ok and x_ok)
+            d = {"scene": first + s}
+            if free:
+                d.update({"bmin8_bit_exact": bool(keys_ok), "residuals_bit_exact": bool(resid_ok)})
+            else:
+                d["cube_bit_exact"] = bool(cube_ok)
+            d.update({"assignment_equal": bool(lsap_ok), "matches": k,
+                      "matches_equal_in_order": bool(match_ok), "costs_bit_exact": bool(cost_ok),
+                      "X_within_1e-10": bool(x_ok)})
+            detail.append(d)
     if not env.is_root:
-        return
+        return None, parity_ok
     total = n_local * world if args.scaling == "weak" else wl["n_scenes"]
-    value = total * args.steps / elapsed
+    value = total * steps / elapsed
     counts = batch.counts()
+    N, M, P = (counts[:, q].astype(np.float64) for q in range(3))
+    triples = float((N * M * P).sum())
     cb = cube_bytes(counts)
-    # the assignment's streamed input: the cube's 8-row minima (default), or
-    # every cost entry once (--lsap-input cost: the floor for a solver that
-    # reads the cost itself)
-    cost_bytes = 4.0 * float((counts[:, 0] * counts[:, 1] * counts[:, 2]).sum())
-    lsap_bytes = 2.0 * float(n_bmin8) if args.lsap_input == "bmin8" else cost_bytes
-    stages = {"cube": (cube_ms, cb, "triplet_fused_kernel"),
+    cost_bytes = 4.0 * triples
+    if free:
+        # the minima pass: centroids + F in, 8-row minima + fp64 residuals out
+        ld = (counts.max() + 3) // 4 * 4
+        first_bytes = (16.0 * counts.sum() + 3 * 72.0 * len(N) + 2.0 * float(n_bmin8)
+                       + 8.0 * float((N * M + P * N + P * M).sum()))
+        lsap_bytes = 2.0 * float(n_bmin8)
+        first_kernel = "triplet_minima_kernel"
+    else:
+        first_bytes = cb
+        # the assignment's streamed input: the cube's 8-row minima (default), or
+        # every cost entry once (--lsap-input cost)
+        lsap_bytes = 2.0 * float(n_bmin8) if lsap_input == "bmin8" else cost_bytes
+        first_kernel = "triplet_fused_kernel"
+    stages = {"cube": (cube_ms, first_bytes, first_kernel),
               "lsap": (lsap_ms, lsap_bytes, "mvm_lsap_solve kernels"),
               "select": (sel_ms, 0.0, "select_triangulate_kernel")}
     dom = max(stages, key=lambda k: stages[k][0])
     d_ms, d_bytes, d_kernel = stages[dom]
     achieved = d_bytes / (d_ms * 1e-3) / 1e9 if d_ms > 0 else None
     cpu = None
-    if args.cpu_seconds > 0:
+    if cpu_seconds > 0:
         threads, threads_src = host_cpu_threads()
         match_cpu_chain(batch, proj, 0, threshold, nthreads=threads)      # warm
         n_cpu, t0 = 0, time.perf_counter()
-        while n_cpu < n_local and time.perf_counter() - t0 < args.cpu_seconds:
+        while n_cpu < n_local and time.perf_counter() - t0 < cpu_seconds:
             match_cpu_chain(batch, proj, n_cpu, threshold, nthreads=threads)
             n_cpu += 1
         secs = time.perf_counter() - t0
@@ -710,29 +790,44 @@ def run_match(args, env, wl, kernel_options):
                           f"x{threads}) + scipy.optimize.linear_sum_assignment (the reference's "
                           "own call, one core) + threshold/sort + numpy SVD per match, on "
                           f"{cpu_model()}")}
+    # the minima pass is fp64-VALU bound: per triple two fp64 adds and one fp64
+    # min (its algorithmic operations), against the MI355X fp64 vector peak
+    valu = None
+    if free and cube_ms > 0:
+        ops_per_s = 3.0 * triples / (cube_ms * 1e-3)
+        valu = {"bound": "fp64 valu", "kernel": "triplet_minima_kernel",
+                "achieved": ops_per_s / 1e12, "peak": 78.6, "unit": "TFLOP/s",
+                "frac": ops_per_s / 1e12 / 78.6, "ops_per_triple": 3,
+                "note": ("algorithmic fp64 operations (two adds and one min per triple; the third "
+                         "and the cast run once per 8 triples and are not counted) over the stage's "
+                         "HIP-event time, against the fp64 vector peak (MI355X_MICROARCH.md)")}
     line = {
         "metric": "captures matched/sec (cost cube + scipy-identical assignment + select/DLT)",
-        "value": value, "unit": "captures/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "value": value, "unit": "captures/s", "n_gpus": world, "steps": steps,
+        "warmup": warmup, "ms_per_step": elapsed / steps * 1e3,
         "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded IPD-like rig, SURVEY §8d generator)",
         "config": {"workload": wl["desc"], "n_cams": 3, "n_dets": wl["n_dets"],
                    "n_scenes_per_gpu": n_local, "n_scenes_total": total,
                    "matching_threshold": threshold, "kernel_options": kernel_options,
-                   "lsap_input": args.lsap_input,
+                   "cube": ("free: 8-row minima + fp64 pair residuals, entries recomputed where read "
+                            "(match_captures keep_cube=False)" if free else
+                            "keep: the cost cubes written and read (keep_cube=True)"),
+                   "lsap_input": "bmin8" if free else lsap_input,
                    "launch": (f"eager op calls, {n_chunks} chunks of scenes: cubes on the launch "
                               "stream, each chunk's assignment + select on a second stream once "
                               "its cube is written" if n_chunks > 1 else "eager op calls, serial"),
                    "match_chunks": n_chunks,
                    "parallelism": f"scene-sharded x{world}" if env.initialised else "single GPU"},
-        "stages_ms": {"cube": cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
+        "stages_ms": {("minima" if free else "cube"): cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
                       "note": ("rank 0, HIP events on each stage's stream, summed over the chunks, "
                                "mean over the timed steps; the stages of different chunks overlap")},
         "lsap": {"problems": n_local, "shape": f"{int(counts[0, 0] * counts[0, 1])} x {int(counts[0, 2])}",
                  "ms_per_batch": lsap_ms, "ms_per_problem": lsap_ms / max(1, n_local),
                  "streamed_gb": lsap_bytes / 1e9, "cost_gb": cost_bytes / 1e9,
-                 "input": ("the cube kernel's 8-row minima (mvm_lsap_solve_ex3)" if args.lsap_input == "bmin8"
-                           else "the cost cubes (mvm_lsap_solve_ex2)")},
+                 "input": ("the 8-row minima + pair residuals (mvm_lsap_solve_resid)" if free
+                           else "the cube kernel's 8-row minima (mvm_lsap_solve_ex3)"
+                           if lsap_input == "bmin8" else "the cost cubes (mvm_lsap_solve_ex2)")},
         "matches_per_step": n_matches,
         "sclk": clocks.summary("sclk"),
         "roofline": {"bound": "hbm", "stage": dom, "kernel": d_kernel, "achieved": achieved,
@@ -740,16 +835,15 @@ def run_match(args, env, wl, kernel_options):
                      "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
                      "bytes_per_launch": d_bytes, "avg_launch_ms": d_ms,
                      "note": ("the slowest stage; its algorithmic bytes: the cube's writes (4 B "
-                              "per triple + 8 B per row + inputs), or for the assignment its "
-                              "streamed input (lsap.streamed_gb)")},
+                              "per triple + 8 B per row + inputs), or free the minima's and "
+                              "residuals' writes, or for the assignment its streamed input "
+                              "(lsap.streamed_gb)")},
+        "valu_roofline": valu,
         "cpu_baseline": cpu,
         "parity": f"{'equal' if parity_ok else 'MISMATCH'} vs the CPU chain on {len(detail)} scenes",
         "parity_detail": detail,
     }
-    print(json.dumps(line), flush=True)
-    if not parity_ok:
-        log("error: c2match parity")
-        raise SystemExit(3)
+    return line, parity_ok
 
 
 def main():
@@ -798,6 +892,15 @@ def main():
                     help="c2match: scenes per step in this many chunks, the assignment of one "
                          "overlapping the cube of the next on a second stream (1: serial, the "
                          "default: the overlap measured slower, DESIGN §11.9)")
+    ap.add_argument("--cube", choices=["free", "keep"], default="free",
+                    help="c2match: free (default, match_captures keep_cube=False): the assignment "
+                         "and the select/DLT recompute the entries they read from the 8-row minima "
+                         "pass's fp64 pair residuals, no cube is written; keep: the cost cubes are "
+                         "written and read")
+    ap.add_argument("--c2match", choices=["auto", "off"], default="auto",
+                    help="auto (default): the c3 workload on one GPU also measures c2match "
+                         "(cube-free) after its own line's parity and nests it in the line as "
+                         "\"c2match\"; off: not")
     ap.add_argument("--lsap-input", choices=["bmin8", "cost"], default="bmin8",
                     help="c2match: the assignment's block minima from the cube kernel's 8-row "
                          "minima (default) or from reading the cost cubes again")
@@ -862,6 +965,11 @@ def main():
         # steps so short that a step's tail and the next one's start matter (C2)
         # take two streams ("steps2": +6-8% on the C2 line)
         args.graph = "steps2" if (args.workload == "c2" and not env.initialised) else "launch"
+    if args.graph == "steps2" and wl["mode"] != "pairwise":
+        # both streams would pass the same plan -- and a workspace-path cube
+        # kernel the same plan.workspace -- to concurrent steps
+        raise SystemExit("--graph steps2 is for the pairwise workloads (c3, c2): concurrent cube "
+                         "steps would share the plan's workspace")
     if args.graph in ("steps", "steps2") and env.initialised:
         raise SystemExit("--graph steps/steps2 need a single GPU without a process group "
                          "(the step's gather is a collective)")
@@ -1384,12 +1492,35 @@ def main():
         out["roofline"]["per_slot"] = per_slot
     if traffic:
         out["roofline"]["traffic_source"] = traffic.get("source")
+    # ---- the association the reference returns, under the same clock: the
+    # default C3 run on one GPU also times c2match (cube-free, the product path
+    # of match_captures) after the C3 line's own parity, with its own parity
+    # against the CPU chain, nested in this line ----------
+    nested_ok = True
+    if args.workload == "c3" and world == 1 and args.c2match == "auto":
+        out_slots.clear()                 # C3's 253 GB of output allocations
+        chunks.clear()
+        graphs = step_graph = gatherer = None
+        argmin = minval = alt_rows = None
+        torch.cuda.synchronize(dev)
+        torch.cuda.empty_cache()
+        t0 = time.perf_counter()
+        nested, nested_ok = match_line(args, env, dict(WORKLOADS["c2match"]), None, steps=20, warmup=3,
+                                       cube_mode="free", cpu_seconds=min(args.cpu_seconds, 5.0))
+        nested["wall_s"] = time.perf_counter() - t0
+        nested["note"] = ("BASELINE configs[1]'s association (C2: 1,000 captures x 3 x 256, what "
+                          "match_objects returns), run after this line's timed region on the same "
+                          "GPU; its own steps, clock and parity")
+        out["c2match"] = nested
     print(json.dumps(out), flush=True)
     if parity_detail and parity_detail["rows_bit_exact"] != parity_detail["rows_checked"]:
         log(f"error: association parity {parity_rows}")
         raise SystemExit(3)
     if not parity_ok:
         log(f"error: residual parity {parity}")
+        raise SystemExit(3)
+    if not nested_ok:
+        log("error: c2match parity (nested)")
         raise SystemExit(3)
 
 

@@ -114,6 +114,10 @@ SIGNATURES = {
         _vp, _vp, _vp, _vp, _vp,
         _vp, _vp,                           # bmin8, bmin8_offs
         _vp, _sz, _vp, _vp]),               # workspace, bytes, options (host), stream
+    "mvm_triplet_minima": (ctypes.c_int, [
+        _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
+        _vp, _vp,                           # bmin8, bmin8_offs
+        _vp, _sz, _vp, _vp]),               # resid, resid_bytes, options (host), stream
     "mvm_lsap_plan": (_i64, [_i32, _vp, _vp, _vp, _vp]),
     "mvm_lsap_plan_ex": (_i64, [_i32, _vp, _vp, _i32, _vp, _vp]),
     "mvm_lsap_solve": (ctypes.c_int, [
@@ -136,6 +140,14 @@ SIGNATURES = {
         _vp, _sz, _vp, _vp, _vp,
         _i64, _i64, _i64,
         _vp, _vp, _vp, _vp, _vp]),          # bmin8, bmin8_offs, segs, options, stream
+    "mvm_lsap_plan_resid": (_i64, [_i32, _vp, _vp, _vp, _vp]),
+    "mvm_lsap_sparse_bounds": (None, [_vp, _vp, _vp]),
+    "mvm_lsap_solve_resid": (ctypes.c_int, [
+        _vp, _i32, _vp, _vp,                # dims, n, ws_offs, out_offs
+        _vp, _sz, _vp, _vp, _vp,            # workspace, bytes, row_ind, col_ind, status
+        _i64, _i64, _i64,                   # long_min, long_max, short_max
+        _vp, _vp, _vp,                      # bmin8, bmin8_offs, segs
+        _vp, _i32, _vp, _vp]),              # resid, max_n, options (host), stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img
         ctypes.c_float, ctypes.c_float,     # conf_thresh, class_id
@@ -144,6 +156,10 @@ SIGNATURES = {
         _vp, _vp, _vp, _i32, _i32, _vp, _vp]),  # proj, set_of_point, pts2d, n_points, n_views, X, stream
     "mvm_select_triangulate": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _vp, _vp,       # cube, cube_offs, cam_offs, lsap_out_offs, row_ind, col_ind
+        _vp, _vp, _i32, ctypes.c_double,    # pts, proj, n_scenes, threshold
+        _vp, _vp, _vp, _vp, _vp]),          # match, cost, X, count, stream
+    "mvm_select_triangulate_resid": (ctypes.c_int, [
+        _vp, _i32, _vp, _vp, _vp, _vp,      # resid, max_n, cam_offs, lsap_out_offs, row_ind, col_ind
         _vp, _vp, _i32, ctypes.c_double,    # pts, proj, n_scenes, threshold
         _vp, _vp, _vp, _vp, _vp]),          # match, cost, X, count, stream
     "mvm_hbm_write_probe": (ctypes.c_int, [_vp, _sz, _vp]),

@@ -71,9 +71,9 @@ extern "C" {
 
 // tools/build_variant.py names its A/B builds (some compute wrong results by design)
 #ifdef MVM_VARIANT
-const char *mvm_version(void) { return "mvmatch 0.6.0 gfx950 variant " MVM_VARIANT; }
+const char *mvm_version(void) { return "mvmatch 0.7.0 gfx950 variant " MVM_VARIANT; }
 #else
-const char *mvm_version(void) { return "mvmatch 0.6.0 gfx950"; }
+const char *mvm_version(void) { return "mvmatch 0.7.0 gfx950"; }
 #endif
 
 const char *mvm_last_error_string(void) { return g_err; }

@@ -134,9 +134,7 @@ __global__ __launch_bounds__(kThreads) void triplet_kernel(CubeArgs args) {
 }
 
 // ------------------------------------------------- fast triplet kernel ----
-constexpr double kThird = 1.0 / 3.0;
-// residual bound under which a sum of three is finite (tile-wide fast path)
-constexpr double kTameResidual = 0x1p1020;
+// (third_q / third_ok / cube_f32 / kTameResidual: mvm_device.h)
 
 // 4 consecutive doubles at a 16-byte aligned address (two dwordx4 loads);
 // lanes past the view's end read zeros.
@@ -153,24 +151,6 @@ __device__ __forceinline__ void load4(const double *p, int valid, double out[4])
         for (int q = 0; q < 4; ++q) out[q] = q < valid ? p[q] : 0.0;
     }
 }
-
-// RN(s / 3) by one Markstein correction (the default): with y = RN(1/3) and
-// q0 = RN(s * y) within one ulp of s/3, r = fma(-q0, 3, s) is exact and
-// q1 = fma(r, y, q0) is the correctly rounded quotient -- for every finite s
-// (checked against the IEEE division on 1.1e9 random, binade-edge,
-// subnormal and near-midpoint inputs, tools/probes/third_markstein.c, and in
-// tests/test_host_logic.py).  Three fp64 ops and a finiteness test instead
-// of a product plus a float32-midpoint/range test (~8 ops, measured 12%
-// slower at 256^3); only non-finite sums (inf: q1 = NaN) take the division.
-// A sum of residuals is never -0, the one input whose sign the correction
-// would not keep.
-__device__ __forceinline__ double third_q(double s) {
-    const double q0 = s * kThird;
-    return __builtin_fma(__builtin_fma(-q0, 3.0, s), kThird, q0);
-}
-
-// true: third_q(s) == RN(s / 3); false: the caller divides
-__device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q); }
 
 // One lane's 16 bytes of a cube row.  `lined`: every row starts on a 128-byte
 // line (P and the scene's offset multiples of 32) -> nontemporal; otherwise a
@@ -1306,17 +1286,6 @@ __host__ __device__ inline size_t small_lds_bytes(int nmax, int ib) {
            6 * (size_t)nmax;
 }
 
-__device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
-    const double sum = (e12 + e13) + e23;
-    double q = third_q(sum);
-    if (!third_ok(q)) {   // non-finite sum: the IEEE division, skipped when no lane needs it
-        double s2 = sum;
-        __asm__ volatile("" : "+v"(s2));   // keeps the division inside the branch (no if-conversion)
-        q = s2 / 3.0;
-    }
-    return (float)q;
-}
-
 __global__ __launch_bounds__(kThreads) void triplet_small_kernel(CubeSmallArgs args) {
     extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
     const int nmax = args.max_n, IB = args.ib;
@@ -1511,6 +1480,286 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
     }
 }
 
+// --------------------------------------- cube-free 8-row minima (ABI 7) ----
+// For an assignment that never reads the cube itself (match_captures with
+// keep_cube=False, bench.py c2match): the 16-bit 8-row minima the fused
+// kernel writes next to the cube (CubeFusedArgs::bmin8), bit for bit, but
+// no cube -- plus every scene's fp64 pair residuals, from which the
+// assignment's kernels recompute the few entries they read (cube_f32):
+//   e12  [N][ld]  at resid + s * stride                  (i, j)
+//   e13T [P][ld]  at resid + s * stride + max_n * ld     (k, i)
+//   e23T [P][ld]  at resid + s * stride + 2 * max_n * ld (k, j)
+// stride = 3 * max_n * ld, ld = roundup(max_n, 4): mvm_triplet_workspace_bytes.
+// RN(s / 3) and the float32 cast are monotone, so the minimum over a group's
+// 8 j of float32(third(s_j)) is float32(third(min_j s_j)): where every
+// residual of a chunk is <= 2^1020 (finite sums) a triple costs two fp64 adds
+// and one fp64 min, and the third runs once per (group, k) -- a quarter of the
+// fused kernel's VALU per triple and none of its 4 B/triple of stores.  Other
+// chunks compute every entry with cube_f32 and take the minimum of the keys
+// (NaN -> key 0), as the fused kernel does.
+// A workgroup owns (scene, 32 consecutive j: one 8-row group per wave) and
+// walks the scene's i rows in chunks of IB, so the wave's e23 registers (8 j x
+// 4 k per lane, the prologue's largest part) are computed once per 256 i rows
+// instead of once per 16; per chunk the e13 [IB][P] and e12 [IB][32] tiles go
+// through LDS (every residual with row_safe's arithmetic, like the fused
+// kernel's prologue).  The workgroups of j block 0 write e13T; every one writes
+// its e23T rows and e12 columns.
+struct MinimaArgs {
+    const double *pts;
+    const int64_t *cam_offs;
+    const double *F;            // [S*3, 9]: F12, F13, F23
+    uint16_t *bmin8;
+    const int64_t *bmin8_offs;
+    double *resid;
+    int64_t stride;             // doubles per scene
+    int32_t ld;                 // row stride of e12 / e13T / e23T (multiple of 4)
+    int32_t max_n;
+    int32_t j_blocks;
+};
+
+template <int IB>
+__global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs args) {
+    constexpr int RPW = 8;                     // j rows per wave: one 8-row group
+    constexpr int kJ = kWaves * RPW;           // j per workgroup
+    struct ColRec {
+        LineRec l;
+        double x, y;
+    };
+    __shared__ __attribute__((aligned(16))) double s13[IB][kChunk];   // 32 KiB at IB 16
+    __shared__ __attribute__((aligned(16))) double s12[IB][kJ];
+    __shared__ LineRec s_r13[IB], s_r12[IB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[IB][2], s_p1[kJ][2];
+    static_assert(sizeof(ColRec) * kChunk <= sizeof(s13), "F23 column scratch fits s13");
+    ColRec *s_c23 = reinterpret_cast<ColRec *>(&s13[0][0]);
+
+    const int t = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
+    const int lane = t % kWave;
+    uint32_t blk = blockIdx.x;   // each XCD a contiguous range of (scene, j block)s
+    {
+        const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
+        blk = x * q + min(x, r) + blk / 8;
+    }
+    const int s = (int)(blk / (uint32_t)args.j_blocks);
+    const int jb = (int)(blk % (uint32_t)args.j_blocks);
+    const int64_t *co = args.cam_offs + 3 * (int64_t)s;
+    const int64_t c0 = co[0], c1 = co[1], c2 = co[2];
+    const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
+    const int jw0 = jb * kJ;
+    if (jw0 >= M || N == 0 || P == 0) return;   // uniform; an empty problem reads no cost
+    const int j0 = jw0 + wave * RPW;
+    const int nrows = min(RPW, M - j0);          // uniform per wave, may be <= 0
+    const int kb = kColsPerLane * lane, kvalid = P - kb;
+    const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
+    const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
+    const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
+    const int ld = args.ld;
+    double *E12 = args.resid + (int64_t)s * args.stride;
+    double *E13T = E12 + (int64_t)args.max_n * ld;
+    double *E23T = E13T + (int64_t)args.max_n * ld;
+    const int g8 = (M + 7) / 8;
+    const int64_t boff = args.bmin8_offs[s];
+    uint16_t *B8 = args.bmin8 + boff;
+    const bool vec = ((P & 3) == 0) && ((boff & 3) == 0);   // 8-byte key stores
+
+    // ---- once per workgroup: the j block's lines and every k column's ----
+    bool any_deg = false;
+    if (t >= kWave && t < kWave + kJ) {
+        const int jj = t - kWave;
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (jw0 + jj < M) {
+            double f[9];
+            px = args.pts[2 * (c1 + jw0 + jj)];
+            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            load_f(F12, f);
+            a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        any_deg |= (a.deg != 0.0) || (b.deg != 0.0);
+        s_c12[jj] = a;
+        s_r23[jj] = b;
+        s_p1[jj][0] = px;
+        s_p1[jj][1] = py;
+    }
+    LineRec cl13{0.0, 0.0, 0.0, 0.0};   // column k = t, F13 (registers, for e13)
+    double kx = 0.0, ky = 0.0;
+    {
+        ColRec c23{{0.0, 0.0, 0.0, 0.0}, 0.0, 0.0};
+        if (t < P) {
+            double f[9];
+            kx = args.pts[2 * (c2 + t)];
+            ky = args.pts[2 * (c2 + t) + 1];
+            load_f(F13, f);
+            cl13.deg = col_line(f, kx, ky, cl13.l0, cl13.l1, cl13.l2) ? 1.0 : 0.0;
+            load_f(F23, f);
+            c23.l.deg = col_line(f, kx, ky, c23.l.l0, c23.l.l1, c23.l.l2) ? 1.0 : 0.0;
+            c23.x = kx;
+            c23.y = ky;
+            any_deg |= (cl13.deg != 0.0) || (c23.l.deg != 0.0);
+        }
+        s_c23[t] = c23;
+    }
+    // uniform: no j / k line of the workgroup is degenerate (the rows' lines
+    // are judged per chunk)
+    const bool deg_fixed = __syncthreads_or(any_deg) != 0;
+    auto pair = [&](bool nd, const LineRec &col, const LineRec &row, double rx, double ry, double cx,
+                    double cy) {
+        if (nd)
+            return 0.5 * (line_dist(col.l0, col.l1, col.l2, rx, ry) +
+                          line_dist(row.l0, row.l1, row.l2, cx, cy));   // :28
+        return pair_e(col, row, rx, ry, cx, cy);
+    };
+    // rows past the view (the last group of a view whose M is not a multiple
+    // of 8) hold e23 = +inf: their sums are +inf (or NaN where a valid row of
+    // the same k is NaN too), so they never decide a group's minimum and the
+    // loops below need no per-row test
+    bool tame23 = true;   // every e23 of this thread's rows is <= kTameResidual
+    double a23[RPW][kColsPerLane];
+#pragma unroll
+    for (int q = 0; q < kColsPerLane; ++q) {
+        const ColRec cl = s_c23[min(kb + q, kChunk - 1)];
+#pragma unroll
+        for (int r = 0; r < RPW; ++r) {
+            const int jj = wave * RPW + r;
+            a23[r][q] = r >= nrows  ? (double)INFINITY
+                        : kb + q < P ? pair(!deg_fixed, cl.l, s_r23[jj], s_p1[jj][0], s_p1[jj][1], cl.x, cl.y)
+                                     : 0.0;
+            tame23 &= r >= nrows || a23[r][q] <= kTameResidual;
+        }
+    }
+    // e23T rows k = kb + q, columns j0 .. j0 + 7 (64 contiguous bytes)
+    if (nrows > 0) {
+#pragma unroll
+        for (int q = 0; q < kColsPerLane; ++q) {
+            if (kb + q >= P) continue;
+            double *dst = E23T + (int64_t)(kb + q) * ld + j0;
+            if (nrows == RPW) {
+#pragma unroll
+                for (int r = 0; r < RPW; r += 2)
+                    *reinterpret_cast<f64x2 *>(dst + r) = f64x2{a23[r][q], a23[r + 1][q]};
+            } else {
+#pragma unroll
+                for (int r = 0; r < RPW; ++r)
+                    if (r < nrows) dst[r] = a23[r][q];
+            }
+        }
+    }
+    __syncthreads();   // every wave has read its F23 columns: s13 is free for e13
+
+    // ---- the scene's i rows, IB at a time ------------------------------------
+    for (int i0 = 0; i0 < N; i0 += IB) {
+        const int ni = min(IB, N - i0);
+        bool deg_rows = false;
+        if (t < IB) {
+            LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+            double px = 0.0, py = 0.0;
+            if (t < ni) {
+                double f[9];
+                px = args.pts[2 * (c0 + i0 + t)];
+                py = args.pts[2 * (c0 + i0 + t) + 1];
+                load_f(F13, f);
+                a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+                load_f(F12, f);
+                b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+            }
+            deg_rows = (a.deg != 0.0) || (b.deg != 0.0);
+            s_r13[t] = a;
+            s_r12[t] = b;
+            s_p0[t][0] = px;
+            s_p0[t][1] = py;
+        }
+        // (the barrier also puts every wave past the previous chunk's reads of
+        // s13 / s12: it must run whatever deg_fixed is -- no short circuit)
+        const bool deg_chunk = __syncthreads_or(deg_rows) != 0;
+        const bool nd = !deg_fixed && !deg_chunk;
+        bool tame = tame23;
+        if (t < P) {
+#pragma unroll 2
+            for (int r = 0; r < IB; r += 2) {
+                const double ea =
+                    r < ni ? pair(nd, cl13, s_r13[r], s_p0[r][0], s_p0[r][1], kx, ky) : 0.0;
+                const double eb =
+                    r + 1 < ni ? pair(nd, cl13, s_r13[r + 1], s_p0[r + 1][0], s_p0[r + 1][1], kx, ky) : 0.0;
+                s13[r][t] = ea;
+                s13[r + 1][t] = eb;
+                tame &= (ea <= kTameResidual) && (eb <= kTameResidual);
+                if (jb == 0) {                     // e13T row k = t: i0 + r, i0 + r + 1
+                    double *dst = E13T + (int64_t)t * ld + i0 + r;
+                    if (r + 1 < ni) *reinterpret_cast<f64x2 *>(dst) = f64x2{ea, eb};
+                    else if (r < ni) dst[0] = ea;
+                }
+            }
+        } else {
+            for (int r = 0; r < IB; ++r) s13[r][t] = 0.0;   // lanes past P read zeros
+        }
+        for (int x = t; x < IB * kJ; x += kThreads) {
+            const int r = x / kJ, jj = x % kJ;
+            const bool v = r < ni && jw0 + jj < M;
+            const double e =
+                v ? pair(nd, s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1]) : 0.0;
+            s12[r][jj] = e;
+            tame &= e <= kTameResidual;
+            if (v) E12[(int64_t)(i0 + r) * ld + jw0 + jj] = e;
+        }
+        // every sum of the chunk is finite when its residuals are <= 2^1020
+        // (NaN fails the compare): the minimum of the sums, then one third
+        const bool fast = __syncthreads_and(tame) != 0;
+        if (nrows <= 0) continue;                  // uniform per wave (barriers above only)
+        for (int ii = 0; ii < ni; ++ii) {
+            double a13[kColsPerLane];
+            {
+                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
+                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
+                a13[0] = lo.x;
+                a13[1] = lo.y;
+                a13[2] = hi.x;
+                a13[3] = hi.y;
+            }
+            double v12[RPW];
+#pragma unroll
+            for (int r = 0; r < RPW; r += 2) {
+                const f64x2 w = *reinterpret_cast<const f64x2 *>(&s12[ii][wave * RPW + r]);
+                v12[r] = w.x;
+                v12[r + 1] = w.y;
+            }
+            uint32_t key[kColsPerLane];
+            if (fast) {
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    double m = (v12[0] + a13[q]) + a23[0][q];          // (e12 + e13) + e23, :81
+#pragma unroll
+                    for (int r = 1; r < RPW; ++r) m = fmin(m, (v12[r] + a13[q]) + a23[r][q]);
+                    key[q] = __float_as_uint((float)third_q(m)) | 0x80000000u;
+                }
+            } else {   // a chunk with a huge / non-finite residual: every entry exactly
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q) {
+                    uint32_t kk = 0xFFFFFFFFu;
+#pragma unroll
+                    for (int r = 0; r < RPW; ++r) {
+                        const double sum = (v12[r] + a13[q]) + a23[r][q];
+                        double qv = third_q(sum);
+                        qv = third_ok(qv) ? qv : sum / 3.0;
+                        kk = umin(kk, bm8_key((float)qv));
+                    }
+                    key[q] = kk;
+                }
+            }
+            uint16_t *brow = B8 + ((int64_t)(i0 + ii) * g8 + j0 / 8) * P;
+            if (vec && kvalid >= kColsPerLane) {
+                *reinterpret_cast<uint2 *>(brow + kb) =
+                    make_uint2((key[0] >> 16) | (key[1] & 0xFFFF0000u), (key[2] >> 16) | (key[3] & 0xFFFF0000u));
+            } else {
+#pragma unroll
+                for (int q = 0; q < kColsPerLane; ++q)
+                    if (q < kvalid) brow[kb + q] = (uint16_t)(key[q] >> 16);
+            }
+        }
+    }
+}
+
 int cube_launch(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                 int32_t n_scenes, int32_t max_n, const int64_t *cube_offs_dev,
                 const int64_t *row_offs_dev, float *cube_dev, int32_t *argmin_dev, float *minval_dev,
@@ -1588,6 +1837,44 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
     return mvm_triplet_cost_argmin_bmin8(pts_dev, cam_offs_dev, F_dev, n_scenes, max_n, cube_offs_dev,
                                          row_offs_dev, cube_dev, argmin_dev, minval_dev, nullptr, nullptr,
                                          workspace_dev, workspace_bytes, opts, stream);
+}
+
+int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
+                       int32_t n_scenes, int32_t max_n, uint16_t *bmin8_dev,
+                       const int64_t *bmin8_offs_dev, double *resid_dev, size_t resid_bytes,
+                       const mvm_options *opts, mvm_stream_t stream) {
+    mvm_clear_error();
+    mvm_options o;
+    int st = mvm_resolve_options(opts, o);
+    if (st) return st;
+    if (n_scenes < 0 || max_n < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative sizes");
+    if (max_n > kChunk)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "mvm_triplet_minima: views of at most %d detections "
+                        "(%d given)", kChunk, (int)max_n);
+    if (n_scenes == 0 || max_n == 0) return MVM_OK;
+    if (!pts_dev || !cam_offs_dev || !F_dev || !bmin8_dev || !bmin8_offs_dev || !resid_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    const size_t need = mvm_triplet_workspace_bytes(n_scenes, max_n);
+    if (resid_bytes < need)
+        return mvm_fail(MVM_ERR_WORKSPACE, "residual workspace %zu bytes < required %zu", resid_bytes, need);
+    if (((uintptr_t)resid_dev & 15) != 0)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "residual workspace not 16-byte aligned");
+    MinimaArgs a{};
+    a.pts = pts_dev;
+    a.cam_offs = cam_offs_dev;
+    a.F = F_dev;
+    a.bmin8 = bmin8_dev;
+    a.bmin8_offs = bmin8_offs_dev;
+    a.resid = resid_dev;
+    a.ld = (max_n + 3) / 4 * 4;
+    a.max_n = max_n;
+    a.stride = (int64_t)3 * max_n * a.ld;
+    a.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+    const int64_t blocks = (int64_t)n_scenes * a.j_blocks;
+    if ((st = grid_check(blocks))) return st;
+    triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0,
+                                reinterpret_cast<hipStream_t>(stream)>>>(a);
+    return mvm_check_launch("triplet_minima_kernel");
 }
 
 }  // extern "C"

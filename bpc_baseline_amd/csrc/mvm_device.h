@@ -306,6 +306,46 @@ __device__ __forceinline__ double half_for_f32(double s) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | (uint32_t)b));
 }
 
+// ------------------------------------------------------- the cube value ----
+constexpr double kThird = 1.0 / 3.0;
+// residual bound under which a sum of three is finite (tile-wide fast path)
+constexpr double kTameResidual = 0x1p1020;
+
+// RN(s / 3) by one Markstein correction (the default): with y = RN(1/3) and
+// q0 = RN(s * y) within one ulp of s/3, r = fma(-q0, 3, s) is exact and
+// q1 = fma(r, y, q0) is the correctly rounded quotient -- for every finite s
+// (checked against the IEEE division on 1.1e9 random, binade-edge,
+// subnormal and near-midpoint inputs, tools/probes/third_markstein.c, and in
+// tests/test_host_logic.py).  Three fp64 ops and a finiteness test instead
+// of a product plus a float32-midpoint/range test (~8 ops, measured 12%
+// slower at 256^3); only non-finite sums (inf: q1 = NaN) take the division.
+// A sum of residuals is never -0, the one input whose sign the correction
+// would not keep.
+__device__ __forceinline__ double third_q(double s) {
+    const double q0 = s * kThird;
+    return __builtin_fma(__builtin_fma(-q0, 3.0, s), kThird, q0);
+}
+
+// true: third_q(s) == RN(s / 3); false: the caller divides
+__device__ __forceinline__ bool third_ok(double q) { return __builtin_isfinite(q); }
+
+// One cube entry: float32(((e12 + e13) + e23) / 3) (epipolar_matching.py:78-81,
+// :96) for any residuals, NaN / inf included.  Every cube kernel computes
+// exactly this (the fused loops inline it); the cube-free consumers of the
+// assignment (mvm_lsap_sparse.hip, select_triangulate) recompute entries with
+// this function from the fp64 pair residuals, so they read the same bits the
+// cube would hold.
+__device__ __forceinline__ float cube_f32(double e12, double e13, double e23) {
+    const double sum = (e12 + e13) + e23;
+    double q = third_q(sum);
+    if (!third_ok(q)) {   // non-finite sum: the IEEE division, skipped when no lane needs it
+        double s2 = sum;
+        __asm__ volatile("" : "+v"(s2));   // keeps the division inside the branch (no if-conversion)
+        q = s2 / 3.0;
+    }
+    return (float)q;
+}
+
 // Running argmin of one row within one lane: best float32 value + its
 // column.  bidx == 0x7FFFFFFF means "no column yet".  Fast-path values are
 // finite, so `v < best` (strict: first occurrence wins) is the whole rule.

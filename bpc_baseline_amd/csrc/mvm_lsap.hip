@@ -78,11 +78,7 @@ __device__ __forceinline__ bool in_sparse_class(const LsapArgs &a, int64_t R, in
 // lsap_reg_kernel's class: short sides up to this (its row state is in LDS)
 constexpr int kRegMaxShort = 1024;
 constexpr int kRegMaxCols = 4096;      // 512 threads x 8 columns, or 1024 x 4
-// default lower bound of the candidate-list class (mvm_options.lsap_sparse_min_cols):
-// 1000 problems of 4096 x 64 take 1.29 ms with candidate lists against 1.66 with
-// the register-state workgroup; 3136 x 56 1.42 against 1.38, 2304 x 48 1.12
-// against 1.03 (tools/bench_lsap.py, profiles/r05/lsap_sparse/)
-constexpr int kSparseMinCols = 4096;
+// (kSparseMinCols, the candidate-list class's default lower bound: mvm_lsap_sparse.h)
 
 __device__ __forceinline__ bool in_reg_class(const LsapArgs &a, int64_t R, int64_t K) {
     const int64_t lng = R > K ? R : K, sht = R > K ? K : R;
@@ -1984,7 +1980,7 @@ int64_t mvm_lsap_plan_ex(int32_t n_problems, const int64_t *rows, const int64_t 
         // candidate lists of the wide class (mvm_lsap_sparse.h)
         int64_t need = (rows[p] && cols[p]) ? (int64_t)lsap_layout(nr, nc, tr, elem).total : 0;
         if (rows[p] && cols[p] && nc <= kSpMaxCols && nr <= kSpMaxShort) {
-            const int64_t sp = (int64_t)lsap_sparse_layout(nr, nc, elem).total;
+            const int64_t sp = (int64_t)lsap_sparse_layout(nr, nc, elem, tr).total;
             need = sp > need ? sp : need;
         }
         w += need;

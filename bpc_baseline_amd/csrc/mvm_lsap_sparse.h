@@ -13,6 +13,11 @@ constexpr int kSpBlock = 32;         // columns per block minimum
 constexpr int kSpTB = 16;            // default candidate blocks per row: the list holds >= 16 entries
 constexpr int kSpLCap = 128;         // entries per candidate list (more: the row is scanned densely)
 constexpr int kSpTileCols = 2048;    // columns per block-minimum workgroup
+// default lower bound of the class (mvm_options.lsap_sparse_min_cols): 1000
+// problems of 4096 x 64 take 1.29 ms with candidate lists against 1.66 with
+// the register-state workgroup; 3136 x 56 1.42 against 1.38, 2304 x 48 1.12
+// against 1.03 (tools/bench_lsap.py, profiles/r05/lsap_sparse/)
+constexpr int kSparseMinCols = 4096;
 
 struct LsapSparseArgs {
     const void *cost;             // float or double (CT)
@@ -35,7 +40,20 @@ struct LsapSparseArgs {
     const int64_t *bmin8_offs;
     const int64_t *segs;
     int32_t tb;                   // candidate blocks per row (mvm_options.lsap_sparse_blocks)
+    // optional (mvm_lsap_solve_resid, ABI 7): no cost at all -- problem p is
+    // scene p of mvm_triplet_minima, its entries recomputed from the scene's
+    // fp64 pair residuals (e12 [N][ld], e13T [P][ld], e23T [P][ld] at
+    // resid + p * resid_stride) with the cube's arithmetic (cube_f32)
+    const double *resid = nullptr;
+    int64_t resid_stride = 0;     // doubles per scene (3 * max_n * ld)
+    int32_t resid_ld = 0;
+    int32_t resid_rows = 0;       // max_n: e13T starts max_n * ld after e12
 };
+
+// status of a problem that cannot be solved as given (ABI 7): its short side
+// exceeds the launch's short_max, its long side the long_max, or -- cube-free
+// -- it is outside the candidate-list class
+constexpr int32_t kSpStatusBounds = 4;
 
 constexpr int kSpMaxBlocks = 2048;   // block minima per row (32 keys per wave lane)
 
@@ -58,7 +76,8 @@ struct SpLayout {
     size_t flags, bm, lcol, lval, ln, theta, total;
 };
 
-__host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, size_t elem) {
+// tr: the problem is tall (transposed, short side = columns)
+__host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, size_t elem, bool tr) {
     SpLayout y;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -67,9 +86,11 @@ __host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, siz
         return at;
     };
     // blocks per row: ceil(L/32) over the whole long side; with segments
-    // (lsap_sparse_seg) (L/seg) * ceil(seg/32) <= min(kSpMaxBlocks, L)
+    // (lsap_sparse_seg, tall problems only) (L/seg) * ceil(seg/32) <=
+    // min(kSpMaxBlocks, L) -- reserved only where segments can apply (a wide
+    // problem of 24 x 576 would otherwise reserve S * L keys: a copy of its cost)
     const int64_t nbf = (L + kSpBlock - 1) / kSpBlock, nbs = L < kSpMaxBlocks ? L : kSpMaxBlocks;
-    const int64_t nb = nbf > nbs ? nbf : nbs;
+    const int64_t nb = tr && nbs > nbf ? nbs : nbf;
     const int64_t nt = (L + kSpTileCols - 1) / kSpTileCols;
     y.flags = take((size_t)(nt > 32 ? nt : 32) * 4);   // invalid-entry flag per tile
     y.bm = take((size_t)S * nb * elem);              // ordered keys of the block minima

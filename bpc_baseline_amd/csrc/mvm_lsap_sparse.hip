@@ -29,6 +29,7 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "mvm_device.h"
 #include "mvm_internal.h"
 
 #pragma clang fp contract(off)
@@ -148,6 +149,52 @@ __device__ __forceinline__ CT sp_w(const CT *C0, bool tr, int S, int L, int s, i
     return tr ? C0[(int64_t)j * S + s] : C0[(int64_t)s * L + j];
 }
 
+// W[s][j] of problem p, from its cost, or -- a cube-free problem
+// (mvm_lsap_solve_resid) -- recomputed from its scene's fp64 pair residuals
+// with the cube's own arithmetic (cube_f32, mvm_device.h): column j = i * M +
+// jj of the flattened (N*M, P) cube, short-side row s = k, so
+// W[k][i M + jj] = float32(((e12[i][jj] + e13T[k][i]) + e23T[k][jj]) / 3),
+// the bits mvm_triplet_cost_argmin would have stored at cube[i][jj][k]
+template <typename CT>
+struct SpSrc {
+    const CT *C0;
+    const double *e12, *e13t, *e23t;   // e12 != nullptr: the residual form
+    int S, L, M, ld;
+    float rM;
+    bool tr;
+    __device__ __forceinline__ CT at(int s, int j) const {
+        if (e12) {
+            int jj;
+            const int i = sp_div(j, M, rM, jj);
+            return (CT)cube_f32(e12[i * ld + jj], e13t[s * ld + i], e23t[s * ld + jj]);
+        }
+        return sp_w(C0, tr, S, L, s, j);
+    }
+};
+
+// problem p's source; seg = lsap_sparse_seg (the residual form needs it: a
+// cube's M), else the residual form is invalid (ok = false)
+template <typename CT>
+__device__ __forceinline__ SpSrc<CT> sp_src(const LsapSparseArgs &a, int p, bool tr, int S, int L, int seg,
+                                            bool &ok) {
+    SpSrc<CT> c{};
+    c.C0 = reinterpret_cast<const CT *>(a.cost) + (a.cost ? a.cost_offs[p] : 0);
+    c.S = S;
+    c.L = L;
+    c.tr = tr;
+    ok = true;
+    if (a.resid) {
+        ok = seg > 0;
+        c.M = seg > 0 ? seg : 1;
+        c.rM = 1.0f / (float)c.M;
+        c.ld = a.resid_ld;
+        c.e12 = a.resid + (int64_t)p * a.resid_stride;
+        c.e13t = c.e12 + (int64_t)a.resid_rows * a.resid_ld;
+        c.e23t = c.e13t + (int64_t)a.resid_rows * a.resid_ld;
+    }
+    return c;
+}
+
 template <typename CT>
 __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, int32_t n, int32_t tpp) {
     using K = SpKey<CT>;
@@ -165,7 +212,7 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
     const int j0 = w * kSpTileCols;
     if (j0 >= L) return;
     const int j1 = min(j0 + kSpTileCols, L);
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
     unsigned char *ws = a.ws + a.ws_offs[p];
     KT *bm = reinterpret_cast<KT *>(ws + y.bm);
     const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
@@ -301,7 +348,7 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
     const int b0 = w * 64;
     if (b0 >= nb) return;
     const int b1 = min(b0 + 64, nb);
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(float));
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(float), tr);
     unsigned char *ws = a.ws + a.ws_offs[p];
     uint32_t *bm = reinterpret_cast<uint32_t *>(ws + y.bm);
     const uint16_t *B8 = a.bmin8 + a.bmin8_offs[p];
@@ -412,17 +459,19 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
     const bool tr = Kd < R;
     const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
     unsigned char *ws = a.ws + a.ws_offs[p];
     const KT *bm = reinterpret_cast<const KT *>(ws + y.bm);
     int32_t *lcol = reinterpret_cast<int32_t *>(ws + y.lcol);
     CT *lval = reinterpret_cast<CT *>(ws + y.lval);
     int32_t *ln = reinterpret_cast<int32_t *>(ws + y.ln);
     CT *theta_out = reinterpret_cast<CT *>(ws + y.theta);
-    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
     // blocks: 32 columns over the whole long side, or (a cube's) segments of
     // seg columns cut in blocks of 32 (block b = segment b / bps, part b % bps)
     const int seg0 = lsap_sparse_seg(a, p, tr, L), seg = seg0 ? seg0 : L;
+    bool src_ok;
+    const SpSrc<CT> src = sp_src<CT>(a, p, tr, S, L, seg0, src_ok);
+    if (!src_ok) return;                                   // sp_solve_kernel reports it
     const int bps = (seg + kSpBlock - 1) / kSpBlock, nb = (L / seg) * bps;
     const float rbps = 1.0f / (float)bps;
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
@@ -524,7 +573,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                     const int cb = idx < nent ? ent[idx] : 0;
                     const int j = (cb & 0xFFFF) + (lane & emask);
                     col[u] = (lane & emask) < (cb >> 16) ? j : -1;
-                    val[u] = col[u] >= 0 ? sp_w(C0, tr, S, L, s, j) : (CT)0;
+                    val[u] = col[u] >= 0 ? src.at(s, j) : (CT)0;
                 }
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -600,17 +649,29 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
         if (threadIdx.x == 0) a.status[p] = 0;
         return;
     }
-    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
+    if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) {
+        // cube-free: nothing else can solve it (there is no cost to read)
+        if (a.resid && threadIdx.x == 0) a.status[p] = kSpStatusBounds;
+        return;
+    }
     const bool tr = Kd < R;
     const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
     const int cap = a.s_cap;
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT));
+    // the LDS was sized by the launch's bounds (short_max -> cap and the slots
+    // per thread, long_max -> the bitmaps' lw words): a problem past them
+    // would write out of range or drop slots; refuse it
+    bool src_ok;
+    const SpSrc<CT> src = sp_src<CT>(a, p, tr, S, L, lsap_sparse_seg(a, p, tr, L), src_ok);
+    if (S > cap || L > 32 * lw || (KS == 1 && S > kSpNT) || !src_ok) {
+        if (threadIdx.x == 0) a.status[p] = kSpStatusBounds;
+        return;
+    }
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
     const unsigned char *ws = a.ws + a.ws_offs[p];
     const int32_t *lcol = reinterpret_cast<const int32_t *>(ws + y.lcol);
     const CT *lval = reinterpret_cast<const CT *>(ws + y.lval);
     const int32_t *ln = reinterpret_cast<const int32_t *>(ws + y.ln);
     const CT *theta = reinterpret_cast<const CT *>(ws + y.theta);
-    const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
 
     uint32_t *s_asg = reinterpret_cast<uint32_t *>(s_dyn);   // [lw] assigned columns
@@ -686,7 +747,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
 #pragma unroll
             for (int m = 0; m < KS; ++m) {
                 const int q = t + kSpNT * m;
-                cv[m] = (q < na && !((rem >> m) & 1u)) ? sp_w(C0, tr, S, L, i, col[m]) : (CT)0;
+                cv[m] = (q < na && !((rem >> m) & 1u)) ? src.at(i, col[m]) : (CT)0;
             }
             int lc = 0;
             CT lv = (CT)0;
@@ -763,7 +824,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                     for (int u = 0; u < 8; ++u) {
                         const int j = j0 + kSpNT * u;
                         ok[u] = j < L && !asg(j);
-                        c[u] = ok[u] ? sp_w(C0, tr, S, L, i, j) : (CT)0;
+                        c[u] = ok[u] ? src.at(i, j) : (CT)0;
                     }
 #pragma unroll
                     for (int u = 0; u < 8; ++u)
@@ -809,7 +870,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                             for (int u = 0; u < 8; ++u) {
                                 const int j = j0 + kSpNT * u;
                                 ok[u] = j < L && !asg(j) && !mvd(j);
-                                c[u] = ok[u] ? sp_w(C0, tr, S, L, is, j) : (CT)0;
+                                c[u] = ok[u] ? src.at(is, j) : (CT)0;
                             }
 #pragma unroll
                             for (int u = 0; u < 8; ++u) {
@@ -823,7 +884,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                     }
                     for (int mm = t; mm < n_mv; mm += kSpNT) {   // free columns off their default place
                         const int c = s_mvc[mm];
-                        if (rfree(mp, sp_w(C0, tr, S, L, is, c), us) == lowest) {
+                        if (rfree(mp, src.at(is, c), us) == lowest) {
                             const long long kk = ((long long)s_mvp[mm] << 16) | c;
                             key = kk > key ? kk : key;
                         }
@@ -951,8 +1012,11 @@ int sp_launch(const LsapSparseArgs &a0, int32_t n, int64_t long_max, hipStream_t
         a.bmin8 = nullptr;
         a.bmin8_offs = nullptr;
         a.segs = nullptr;
+        a.resid = nullptr;
     }
-    sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
+    // cube-free: every problem of the class takes its block minima from the
+    // 8-row minima (a problem that cannot is refused by sp_solve_kernel)
+    if (!a.resid) sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
     if (a.bmin8)
         sp_bmin8_reduce_kernel<<<dim3((unsigned)(n * (kSpMaxBlocks / 64))), dim3(kSpNT), 0, s>>>(a, n);
     sp_lists_kernel<CT><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
@@ -980,3 +1044,94 @@ int lsap_sparse_launch_f32(const LsapSparseArgs &a, int32_t n, int64_t long_max,
 int lsap_sparse_launch_f64(const LsapSparseArgs &a, int32_t n, int64_t long_max, hipStream_t s) {
     return sp_launch<double>(a, n, long_max, s);
 }
+
+// ================================================================ C ABI ====
+extern "C" {
+
+void mvm_lsap_sparse_bounds(int32_t *min_cols, int32_t *max_cols, int32_t *max_short) {
+    if (min_cols) *min_cols = kSparseMinCols;
+    if (max_cols) *max_cols = kSpMaxCols;
+    if (max_short) *max_short = kSpMaxShort;
+}
+
+int64_t mvm_lsap_plan_resid(int32_t n_problems, const int64_t *rows, const int64_t *cols,
+                            int64_t *ws_offs, int64_t *out_offs) {
+    if (n_problems < 0 || (n_problems > 0 && (!rows || !cols || !ws_offs || !out_offs))) {
+        mvm_set_error("mvm_lsap_plan_resid: invalid arguments");
+        return -1;
+    }
+    int64_t w = 0, o = 0;
+    for (int32_t p = 0; p < n_problems; ++p) {
+        if (rows[p] < 0 || cols[p] < 0 || rows[p] > 0x7FFFFFFF || cols[p] > 0x7FFFFFFF) {
+            mvm_set_error("mvm_lsap_plan_resid: problem dimensions out of range");
+            return -1;
+        }
+        ws_offs[p] = w;
+        out_offs[p] = o;
+        const bool tr = cols[p] < rows[p];
+        const int64_t nr = tr ? cols[p] : rows[p], nc = tr ? rows[p] : cols[p];
+        // only the candidate-list class's lists (no transposed cost: there is none)
+        if (rows[p] && cols[p] && nc <= kSpMaxCols && nr <= kSpMaxShort)
+            w += (int64_t)lsap_sparse_layout(nr, nc, sizeof(float), tr).total;
+        o += rows[p] < cols[p] ? rows[p] : cols[p];
+    }
+    ws_offs[n_problems] = w;
+    out_offs[n_problems] = o;
+    return w;
+}
+
+int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                         const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                         int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                         int64_t long_min, int64_t long_max, int64_t short_max,
+                         const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                         const int64_t *segs_dev, const double *resid_dev, int32_t max_n,
+                         const mvm_options *opts, mvm_stream_t stream) {
+    mvm_clear_error();
+    mvm_options o;
+    int st = mvm_resolve_options(opts, o);
+    if (st) return st;
+    if (o.lsap_sparse_blocks < 0 || o.lsap_sparse_blocks > 64)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "lsap_sparse_blocks %d not in 0..64",
+                        (int)o.lsap_sparse_blocks);
+    if (n_problems < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative n_problems");
+    if (n_problems == 0) return MVM_OK;
+    if (!dims_dev || !ws_offs_dev || !out_offs_dev || !status_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (max_n < 0 || max_n > kChunk)
+        return mvm_fail(MVM_ERR_UNSUPPORTED, "mvm_lsap_solve_resid: views of at most %d detections "
+                        "(max_n %d)", kChunk, (int)max_n);
+    const int sp_lo = o.lsap_sparse_min_cols == 0 ? kSparseMinCols
+                                                  : (o.lsap_sparse_min_cols < 0 ? 0 : o.lsap_sparse_min_cols);
+    int wave_max = o.lsap_wave_max_cols == 0 ? 1024 : o.lsap_wave_max_cols;
+    wave_max = wave_max < 0 ? 0 : (wave_max > 1024 ? 1024 : wave_max);
+    if (long_max >= 1) {
+        // there is no cost for any other class to read: every non-empty
+        // problem must be the candidate-list class's (tall: P <= 256 < its long side)
+        if (sp_lo <= 0 || long_min < sp_lo || long_min <= wave_max || long_max > kSpMaxCols ||
+            short_max < 1 || short_max > kSpMaxShort)
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT,
+                            "mvm_lsap_solve_resid: long sides [%lld, %lld] / short sides <= %lld are not "
+                            "all of the candidate-list class (long sides >= %d, > %d, <= %d; short sides "
+                            "<= %d)", (long long)long_min, (long long)long_max, (long long)short_max, sp_lo,
+                            wave_max, kSpMaxCols, kSpMaxShort);
+        if (!bmin8_dev || !bmin8_offs_dev || !segs_dev || !resid_dev || !workspace_dev || !row_ind_dev ||
+            !col_ind_dev)
+            return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    }
+    (void)workspace_bytes;   // the per-problem regions come from mvm_lsap_plan_resid's offsets
+    LsapSparseArgs sa{nullptr, nullptr, dims_dev, ws_offs_dev,
+                      reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
+                      col_ind_dev, status_dev, sp_lo > 0 ? sp_lo : 1, wave_max,
+                      (int32_t)(short_max < 1 ? 1 : short_max), bmin8_dev, bmin8_offs_dev, segs_dev,
+                      o.lsap_sparse_blocks ? o.lsap_sparse_blocks : kSpTB};
+    const int ld = (max_n + 3) / 4 * 4;
+    sa.resid = resid_dev;
+    sa.resid_ld = ld;
+    sa.resid_rows = max_n;
+    sa.resid_stride = (int64_t)3 * max_n * ld;
+    return sp_launch<float>(sa, n_problems, long_max < 1 ? 1 : long_max,
+                            reinterpret_cast<hipStream_t>(stream));
+}
+
+}  // extern "C"

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "mvmatch.h"
+#include "mvm_device.h"
 #include "mvm_internal.h"
 
 #pragma clang fp contract(off)
@@ -247,31 +248,58 @@ void launch_dlt(const double *proj, const int32_t *sop, const double *pts2d, int
 constexpr int kSelThreads = 256;
 constexpr int kSelTile = 1024;
 
+// the cube entry (r, k) of scene s: read from the cube, or -- cube-free
+// (mvm_select_triangulate_resid) -- recomputed from the scene's fp64 pair
+// residuals (mvm_triplet_minima's layout) with the cube's own arithmetic
+struct SelSrc {
+    const float *cb;
+    const double *e12, *e13t, *e23t;   // e12 != nullptr: the residual form
+    int64_t M, P;
+    int ld;
+    __device__ __forceinline__ float at(int64_t r, int64_t k) const {
+        if (e12) {
+            const int64_t i = r / M, j = r - i * M;
+            return cube_f32(e12[i * ld + j], e13t[k * ld + i], e23t[k * ld + j]);
+        }
+        return cb[r * P + k];
+    }
+};
+
 __global__ __launch_bounds__(kSelThreads) void select_triangulate_kernel(
     const float *cube, const int64_t *cube_offs, const int64_t *cam_offs,
     const int64_t *lsap_offs, const int64_t *row_ind, const int64_t *col_ind, const double *pts,
     const double *proj, double threshold, int32_t *match, float *cost_out, double *X,
-    int32_t *count) {
+    int32_t *count, const double *resid, int64_t rstride, int32_t rld, int32_t rrows) {
     __shared__ float s_cost[kSelTile];
     __shared__ int s_kept;
     const int s = blockIdx.x, t = threadIdx.x;
     const int64_t o = lsap_offs[s], n = lsap_offs[s + 1] - o;
     const int64_t c0 = cam_offs[3 * s], c1 = cam_offs[3 * s + 1], c2 = cam_offs[3 * s + 2];
     const int64_t M = c2 - c1, P = cam_offs[3 * s + 3] - c2;
-    const float *cb = cube + cube_offs[s];
+    SelSrc cb{};
+    cb.M = M;
+    cb.P = P;
+    if (resid) {
+        cb.ld = rld;
+        cb.e12 = resid + (int64_t)s * rstride;
+        cb.e13t = cb.e12 + (int64_t)rrows * rld;
+        cb.e23t = cb.e13t + (int64_t)rrows * rld;
+    } else {
+        cb.cb = cube + cube_offs[s];
+    }
     if (t == 0) s_kept = 0;
     for (int64_t m0 = 0; m0 < n; m0 += kSelThreads) {
         const int64_t m = m0 + t;
         float mine = INFINITY;
         if (m < n) {
-            const float v = cb[row_ind[o + m] * P + col_ind[o + m]];
+            const float v = cb.at(row_ind[o + m], col_ind[o + m]);
             if ((double)v < threshold) mine = v;
         }
         int64_t rank = 0;
         for (int64_t q0 = 0; q0 < n; q0 += kSelTile) {
             __syncthreads();
             for (int q = t; q < kSelTile && q0 + q < n; q += kSelThreads) {
-                const float v = cb[row_ind[o + q0 + q] * P + col_ind[o + q0 + q]];
+                const float v = cb.at(row_ind[o + q0 + q], col_ind[o + q0 + q]);
                 s_cost[q] = (double)v < threshold ? v : INFINITY;
             }
             __syncthreads();
@@ -367,7 +395,25 @@ int mvm_select_triangulate(const float *cube_dev, const int64_t *cube_offs_dev,
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     select_triangulate_kernel<<<n_scenes, kSelThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
         cube_dev, cube_offs_dev, cam_offs_dev, lsap_out_offs_dev, row_ind_dev, col_ind_dev, pts_dev,
-        proj_dev, threshold, match_dev, cost_dev, X_dev, count_dev);
+        proj_dev, threshold, match_dev, cost_dev, X_dev, count_dev, nullptr, 0, 0, 0);
+    return mvm_check_launch("select_triangulate_kernel");
+}
+
+int mvm_select_triangulate_resid(const double *resid_dev, int32_t max_n, const int64_t *cam_offs_dev,
+                                 const int64_t *lsap_out_offs_dev, const int64_t *row_ind_dev,
+                                 const int64_t *col_ind_dev, const double *pts_dev,
+                                 const double *proj_dev, int32_t n_scenes, double threshold,
+                                 int32_t *match_dev, float *cost_dev, double *X_dev, int32_t *count_dev,
+                                 mvm_stream_t stream) {
+    mvm_clear_error();
+    if (n_scenes < 0 || max_n < 0) return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "negative sizes");
+    if (n_scenes == 0) return MVM_OK;
+    if (!resid_dev || !cam_offs_dev || !lsap_out_offs_dev || !proj_dev || !count_dev)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    const int32_t ld = (max_n + 3) / 4 * 4;
+    select_triangulate_kernel<<<n_scenes, kSelThreads, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        nullptr, nullptr, cam_offs_dev, lsap_out_offs_dev, row_ind_dev, col_ind_dev, pts_dev, proj_dev,
+        threshold, match_dev, cost_dev, X_dev, count_dev, resid_dev, (int64_t)3 * max_n * ld, ld, max_n);
     return mvm_check_launch("select_triangulate_kernel");
 }
 

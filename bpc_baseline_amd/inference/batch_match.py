@@ -130,26 +130,18 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
     np.cumsum(counts_host, out=cam_offs_host[1:])
     mark("counts D2H")
 
-    plan = ops.TripletPlan(cam_offs_host, S, device=dev)
     c3 = counts_host.reshape(S, 3)
-    # flattened cubes of >= 4096 rows go to the candidate-list assignment:
-    # the cube kernel then also writes the 8-row minima it reduces
-    bm8 = None
-    if S and int((c3[:, 0] * c3[:, 1]).max()) >= 4096:
-        bm8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=dev)
-    mark("cube plan")
-    cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan, bmin8=bm8)
-    mark("cube")
-    lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
-    mark("lsap plan")
-    row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(
-        cube, plan.cube_offs[:-1].contiguous(), lplan,
-        bmin8=(bm8, plan.bmin8_offs, plan.segs) if bm8 is not None else None)
-    mark("lsap")
-    match, cost, X, count = ops.select_triangulate(cube, plan.cube_offs, cam_offs, lplan.out_offs,
-                                                   row_ind, col_ind, pts, proj_dev,
-                                                   float(matching_threshold))
-    mark("select")
+    free = ops.cube_free_scenes(c3) if not keep_cube else np.zeros(S, bool)
+    if free.all() or not free.any():
+        res = _device_chain(pts, cam_offs, cam_offs_host, F_dev, proj_dev, S, float(matching_threshold),
+                            bool(free.all()) and S > 0, keep_cube, mark)
+    else:
+        # a mixed batch: the scenes of the candidate-list class without the
+        # cube, the others (small views: the dense assignment classes read
+        # the cost) with it; each part is a contiguous sub-batch
+        res = _split_chain(pts, cam_offs_host, F_dev, proj_dev, S, float(matching_threshold), free,
+                           mark)
+    match, cost, X, lstat, count, out_offs_host, cube = res
     # one device -> host copy: assignment statuses and match counts
     sc = torch.cat([lstat, count]).cpu().numpy()
     bad, count_h = sc[:S], sc[S:]
@@ -158,8 +150,92 @@ def match_captures(boxes: torch.Tensor, conf: torch.Tensor, cls: torch.Tensor,
                          "(cost matrix contains invalid numeric entries or is infeasible)")
     mark("results D2H")
     return MatchBatch(match=match, cost=cost, X=X, count=count_h,
-                      offs=lplan.out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
+                      offs=out_offs_host, pts=pts, boxes=boxes_int, cam_offs=cam_offs_host,
                       cube=cube if keep_cube else None)
+
+
+def _device_chain(pts, cam_offs, cam_offs_host, F_dev, proj_dev, S, threshold, cube_free, keep_cube,
+                  mark):
+    """Cube (or, cube_free, its 8-row minima + pair residuals) -> assignment ->
+    select/DLT of S scenes whose CSR offsets are ``cam_offs`` (device) /
+    ``cam_offs_host``.  -> (match, cost, X, status, count, out_offs_host, cube or None)."""
+    dev = pts.device
+    plan = ops.TripletPlan(cam_offs_host, S, device=dev)
+    c3 = plan.counts
+    mark("cube plan")
+    if cube_free:
+        # the assignment never reads a cube: the 8-row minima it reduces and
+        # the fp64 pair residuals it recomputes its entries from (DESIGN §12.1)
+        bm8 = ops.triplet_minima(pts, cam_offs, F_dev, plan)
+        mark("cube")
+        lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
+        mark("lsap plan")
+        row_ind, col_ind, lstat = ops.linear_sum_assignment_resid(lplan, plan, bm8)
+        mark("lsap")
+        match, cost, X, count = ops.select_triangulate_resid(plan, cam_offs, lplan.out_offs, row_ind,
+                                                             col_ind, pts, proj_dev, threshold)
+        mark("select")
+        return match, cost, X, lstat, count, lplan.out_offs_host, None
+    # flattened cubes of the candidate-list class: the cube kernel also writes
+    # the 8-row minima that class reduces (DESIGN §11.2)
+    bm8 = None
+    lo, hi, sh = ops.sparse_class_bounds()
+    nm = c3[:, 0] * c3[:, 1]
+    if S and bool(((nm >= lo) & (nm > 1024) & (nm <= hi) & (c3[:, 2] <= sh) & (nm > c3[:, 2])).any()):
+        bm8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=dev)
+    cube, _, _ = ops.triplet_cost_argmin(pts, cam_offs, F_dev, plan, bmin8=bm8)
+    mark("cube")
+    lplan = ops.LsapPlan(nm, c3[:, 2], device=dev)
+    mark("lsap plan")
+    row_ind, col_ind, lstat = ops.linear_sum_assignment_batched(
+        cube, plan.cube_offs[:-1].contiguous(), lplan,
+        bmin8=(bm8, plan.bmin8_offs, plan.segs) if bm8 is not None else None)
+    mark("lsap")
+    match, cost, X, count = ops.select_triangulate(cube, plan.cube_offs, cam_offs, lplan.out_offs,
+                                                   row_ind, col_ind, pts, proj_dev, threshold)
+    mark("select")
+    return match, cost, X, lstat, count, lplan.out_offs_host, (cube if keep_cube else None)
+
+
+def _split_chain(pts, cam_offs_host, F_dev, proj_dev, S, threshold, free, mark):
+    """_device_chain over the cube-free scenes and the others as two
+    contiguous sub-batches (their centroids, F and P gathered on the device),
+    merged back into the batch's scene order and assignment offsets."""
+    dev = pts.device
+    co = np.asarray(cam_offs_host, np.int64)
+    c3 = np.diff(co).reshape(S, 3)
+    caps = np.minimum(c3[:, 0] * c3[:, 1], c3[:, 2])
+    out_offs = np.zeros(S + 1, np.int64)
+    np.cumsum(caps, out=out_offs[1:])
+    cap = int(out_offs[-1])
+    match = torch.zeros((max(cap, 1), 3), dtype=torch.int32, device=dev)
+    cost = torch.zeros(max(cap, 1), dtype=torch.float32, device=dev)
+    X = torch.zeros((max(cap, 1), 3), dtype=torch.float64, device=dev)
+    status = torch.zeros(S, dtype=torch.int32, device=dev)
+    count = torch.zeros(S, dtype=torch.int32, device=dev)
+    F3 = F_dev.reshape(S, 27)
+    for part in (np.nonzero(free)[0], np.nonzero(~free)[0]):
+        if part.size == 0:
+            continue
+        rows = np.concatenate([np.arange(co[3 * s], co[3 * s + 3]) for s in part]).astype(np.int64)
+        sub_co = np.zeros(3 * part.size + 1, np.int64)
+        np.cumsum(c3[part].reshape(-1), out=sub_co[1:])
+        sel, idx, dst_rows, src_rows, sub_co_dev = ops._h2d_int64(
+            [rows, part.astype(np.int64),
+             np.concatenate([np.arange(out_offs[s], out_offs[s] + caps[s]) for s in part]).astype(np.int64),
+             np.arange(int(caps[part].sum()), dtype=np.int64), sub_co], dev)
+        sub_pts = pts.index_select(0, sel) if rows.size else pts[:0]
+        m, c, x, st, n, _, _ = _device_chain(sub_pts, sub_co_dev, sub_co,
+                                             F3.index_select(0, idx).reshape(-1),
+                                             proj_dev.index_select(0, idx), part.size, threshold,
+                                             bool(free[part[0]]), False, mark)
+        if src_rows.numel():
+            match.index_copy_(0, dst_rows, m.index_select(0, src_rows))
+            cost.index_copy_(0, dst_rows, c.index_select(0, src_rows))
+            X.index_copy_(0, dst_rows, x.index_select(0, src_rows))
+        status.index_copy_(0, idx, st)
+        count.index_copy_(0, idx, n)
+    return match[:cap], cost[:cap], X[:cap], status, count, out_offs, None
 
 
 def _rig_inputs(batch: Sequence):

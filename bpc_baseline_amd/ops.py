@@ -35,6 +35,8 @@ __all__ = [
     "pairwise_residual_argmin", "pairwise_residual_f64", "triplet_cost_argmin",
     "hbm_write_probe", "LsapPlan", "linear_sum_assignment_batched",
     "pack_detections", "triangulate_dlt", "select_triangulate",
+    "triplet_minima", "linear_sum_assignment_resid", "select_triangulate_resid",
+    "cube_free_scenes", "sparse_class_bounds",
 ]
 
 
@@ -272,6 +274,59 @@ def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, sta
     return None
 
 
+@torch.library.custom_op("mvmatch::triplet_minima_out", mutates_args=("bmin8", "resid"))
+def triplet_minima_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, max_n: int,
+                       bmin8: Tensor, bmin8_offs: Tensor, resid: Tensor,
+                       opts: Optional[List[int]] = None) -> None:
+    """The cube's 8-row minima + every scene's fp64 pair residuals, no cube
+    (mvm_triplet_minima, ABI 7)."""
+    _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
+    for t, n, dt in ((bmin8, "bmin8", torch.int16), (bmin8_offs, "bmin8_offs", torch.int64),
+                     (resid, "resid", torch.uint8)):
+        _require(t, n, dt, pts.device)
+    st = _native.load().mvm_triplet_minima(_p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(bmin8),
+                                           _p(bmin8_offs), _p(resid), resid.numel(), _opts_ref(opts),
+                                           _stream(pts))
+    _native.check("mvm_triplet_minima", st)
+
+
+@triplet_minima_out.register_fake
+def _(pts, cam_offs, F, n_scenes, max_n, bmin8, bmin8_offs, resid, opts=None):
+    return None
+
+
+@torch.library.custom_op("mvmatch::lsap_solve_resid_out",
+                         mutates_args=("workspace", "row_ind", "col_ind", "status"))
+def lsap_solve_resid_out(dims: Tensor, ws_offs: Tensor, out_offs: Tensor, workspace: Tensor,
+                         row_ind: Tensor, col_ind: Tensor, status: Tensor, bmin8: Tensor,
+                         bmin8_offs: Tensor, segs: Tensor, resid: Tensor, max_n: int, long_min: int,
+                         long_max: int, short_max: int, opts: Optional[List[int]] = None) -> None:
+    """The assignment of every flattened cube of a triplet_minima batch, from
+    its 8-row minima and pair residuals (mvm_lsap_solve_resid, ABI 7)."""
+    dev = dims.device
+    if dev.type != "cuda":
+        raise ValueError("dims must be a GPU tensor (the matcher has no CPU path)")
+    for t, n, dt in ((dims, "dims", torch.int64), (ws_offs, "ws_offs", torch.int64),
+                     (out_offs, "out_offs", torch.int64), (workspace, "workspace", torch.uint8),
+                     (row_ind, "row_ind", torch.int64), (col_ind, "col_ind", torch.int64),
+                     (status, "status", torch.int32), (bmin8, "bmin8", torch.int16),
+                     (bmin8_offs, "bmin8_offs", torch.int64), (segs, "segs", torch.int64),
+                     (resid, "resid", torch.uint8)):
+        _require(t, n, dt, dev)
+    st = _native.load().mvm_lsap_solve_resid(_p(dims), status.numel(), _p(ws_offs), _p(out_offs),
+                                             _p(workspace), workspace.numel(), _p(row_ind), _p(col_ind),
+                                             _p(status), long_min, long_max, short_max, _p(bmin8),
+                                             _p(bmin8_offs), _p(segs), _p(resid), max_n, _opts_ref(opts),
+                                             _stream(dims))
+    _native.check("mvm_lsap_solve_resid", st)
+
+
+@lsap_solve_resid_out.register_fake
+def _(dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, bmin8, bmin8_offs, segs, resid,
+      max_n, long_min, long_max, short_max, opts=None):
+    return None
+
+
 @torch.library.custom_op("mvmatch::pack_detections_out",
                          mutates_args=("counts", "cam_offs", "pts", "boxes_out", "status"))
 def pack_detections_out(boxes: Tensor, conf: Tensor, cls: Tensor, img_offs: Tensor,
@@ -374,6 +429,45 @@ def select_triangulate_out(cube: Tensor, cube_offs: Tensor, cam_offs: Tensor, ls
 @select_triangulate_out.register_fake
 def _(cube, cube_offs, cam_offs, lsap_offs, row_ind, col_ind, pts, proj, threshold, match, cost,
       X, count):
+    return None
+
+
+@torch.library.custom_op("mvmatch::select_triangulate_resid_out",
+                         mutates_args=("match", "cost", "X", "count"))
+def select_triangulate_resid_out(resid: Tensor, max_n: int, cam_offs: Tensor, lsap_offs: Tensor,
+                                 row_ind: Tensor, col_ind: Tensor, pts: Tensor, proj: Tensor,
+                                 threshold: float, match: Tensor, cost: Tensor, X: Tensor,
+                                 count: Tensor) -> None:
+    """select_triangulate_out with each assigned entry recomputed from a
+    triplet_minima batch's residuals (mvm_select_triangulate_resid, ABI 7)."""
+    dev = pts.device
+    if dev.type != "cuda":
+        raise ValueError("pts must be a GPU tensor (the matcher has no CPU path)")
+    n_scenes = count.numel()
+    for t, name, dt, numel in ((resid, "resid", torch.uint8, 0),
+                               (cam_offs, "cam_offs", torch.int64, 3 * n_scenes + 1),
+                               (lsap_offs, "lsap_offs", torch.int64, n_scenes + 1),
+                               (row_ind, "row_ind", torch.int64, 0), (col_ind, "col_ind", torch.int64, 0),
+                               (pts, "pts", torch.float64, 0), (proj, "proj", torch.float64, 36 * n_scenes),
+                               (match, "match", torch.int32, 3 * row_ind.numel()),
+                               (cost, "cost", torch.float32, row_ind.numel()),
+                               (X, "X", torch.float64, 3 * row_ind.numel()),
+                               (count, "count", torch.int32, 0)):
+        _require(t, name, dt, dev)
+        if numel and t.numel() != numel and name in ("cam_offs", "lsap_offs", "proj"):
+            raise ValueError(f"{name} holds {t.numel()} elements, expected {numel}")
+        if numel and t.numel() < numel:
+            raise ValueError(f"{name} holds {t.numel()} elements, needs {numel}")
+    if col_ind.numel() != row_ind.numel():
+        raise ValueError("row_ind / col_ind differ in length")
+    st = _native.load().mvm_select_triangulate_resid(
+        _p(resid), max_n, _p(cam_offs), _p(lsap_offs), _p(row_ind), _p(col_ind), _p(pts), _p(proj),
+        n_scenes, float(threshold), _p(match), _p(cost), _p(X), _p(count), _stream(pts))
+    _native.check("mvm_select_triangulate_resid", st)
+
+
+@select_triangulate_resid_out.register_fake
+def _(resid, max_n, cam_offs, lsap_offs, row_ind, col_ind, pts, proj, threshold, match, cost, X, count):
     return None
 
 
@@ -545,6 +639,44 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
     return cube, argmin, minval
 
 
+def triplet_minima(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
+                   bmin8: Optional[Tensor] = None, options: Optional[dict] = None):
+    """Cube-free input of the assignment (mvm_triplet_minima, ABI 7): the
+    cube's 8-row minima (int16 [plan.n_bmin8], the same bits
+    ``triplet_cost_argmin(..., bmin8=)`` writes) and every scene's fp64 pair
+    residuals, written into ``plan.workspace`` (which the default cube kernels
+    do not use; a later cube launch on the plan with the workspace kernel
+    would overwrite them).  -> bmin8.  Views of at most 256 detections."""
+    if bmin8 is None:
+        bmin8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=pts.device)
+    torch.ops.mvmatch.triplet_minima_out(pts, cam_offs, F, plan.n_scenes, plan.max_n, bmin8,
+                                         plan.bmin8_offs, plan.workspace, _opts_list(options))
+    return bmin8
+
+
+def sparse_class_bounds() -> Tuple[int, int, int]:
+    """(default lower bound of the long side, largest long side, largest
+    short side) of the candidate-list assignment class (mvm_lsap_sparse_bounds)."""
+    v = [ctypes.c_int32(0) for _ in range(3)]
+    _native.load().mvm_lsap_sparse_bounds(*(ctypes.byref(x) for x in v))
+    return tuple(int(x.value) for x in v)
+
+
+def cube_free_scenes(counts: np.ndarray, min_cols: Optional[int] = None) -> np.ndarray:
+    """Per scene of a (S, 3) count array: True where the cube-free association
+    (triplet_minima -> linear_sum_assignment_resid -> select_triangulate_resid)
+    can take it: an empty problem, or views of <= 256 detections whose
+    flattened (N*M, P) problem is of the candidate-list class."""
+    lo, hi, sh = sparse_class_bounds()
+    lo = lo if min_cols is None else int(min_cols)
+    c = np.asarray(counts, dtype=np.int64).reshape(-1, 3)
+    nm, p = c[:, 0] * c[:, 1], c[:, 2]
+    empty = (nm == 0) | (p == 0)
+    lng, sht = np.maximum(nm, p), np.minimum(nm, p)
+    ok = (c.max(axis=1) <= 256) & (lng >= lo) & (lng > 1024) & (lng <= hi) & (sht <= sh)
+    return empty | ok
+
+
 def hbm_write_probe(buf: Tensor) -> None:
     """Stream 16-byte nontemporal stores over ``buf`` (roofline reference)."""
     if buf.device.type != "cuda" or not buf.is_contiguous():
@@ -560,19 +692,28 @@ class LsapPlan:
     matrix: the workspace holds transposed costs of that type)."""
 
     def __init__(self, rows, cols, device: torch.device | str = "cuda",
-                 dtype: torch.dtype = torch.float32):
+                 dtype: torch.dtype = torch.float32, resid: bool = False):
         rows = np.ascontiguousarray(rows, dtype=np.int64).reshape(-1)
         cols = np.ascontiguousarray(cols, dtype=np.int64).reshape(-1)
         if dtype not in (torch.float32, torch.float64):
             raise ValueError(f"LsapPlan: dtype must be float32 or float64, got {dtype}")
+        if resid and dtype != torch.float32:
+            raise ValueError("LsapPlan: the cube-free form assigns float32 cube entries")
         n = rows.size
         ws_offs = np.zeros(n + 1, np.int64)
         out_offs = np.zeros(n + 1, np.int64)
-        code = _native.MVM_F64 if dtype == torch.float64 else _native.MVM_F32
-        total = _native.load().mvm_lsap_plan_ex(n, rows.ctypes.data, cols.ctypes.data, code,
-                                                ws_offs.ctypes.data, out_offs.ctypes.data)
+        if resid:      # cube-free (mvm_lsap_solve_resid): the candidate lists only
+            fn = "mvm_lsap_plan_resid"
+            total = _native.load().mvm_lsap_plan_resid(n, rows.ctypes.data, cols.ctypes.data,
+                                                       ws_offs.ctypes.data, out_offs.ctypes.data)
+        else:
+            fn = "mvm_lsap_plan_ex"
+            code = _native.MVM_F64 if dtype == torch.float64 else _native.MVM_F32
+            total = _native.load().mvm_lsap_plan_ex(n, rows.ctypes.data, cols.ctypes.data, code,
+                                                    ws_offs.ctypes.data, out_offs.ctypes.data)
         if total < 0:
-            raise _native.MvmError("mvm_lsap_plan_ex", -1, _native.load().mvm_last_error_string().decode())
+            raise _native.MvmError(fn, -1, _native.load().mvm_last_error_string().decode())
+        self.resid = bool(resid)
         self.dtype = dtype
         self.n = n
         self.rows, self.cols = rows, cols
@@ -613,6 +754,26 @@ def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPla
     torch.ops.mvmatch.lsap_solve_out(cost, cost_offs, plan.dims, plan.ws_offs, plan.out_offs,
                                      plan.workspace, row_ind, col_ind, status, plan.long_min,
                                      plan.long_max, _opts_list(options), plan.short_max)
+    return row_ind[:plan.n_out], col_ind[:plan.n_out], status
+
+
+def linear_sum_assignment_resid(plan: LsapPlan, tplan: TripletPlan, bmin8: Tensor, *,
+                                options: Optional[dict] = None):
+    """linear_sum_assignment_batched of every flattened (N*M, P) cube of a
+    ``triplet_minima(..., tplan)`` batch without the cubes (mvm_lsap_solve_resid):
+    the same result (scipy's).  ``plan`` = LsapPlan(N*M, P, resid=True).
+    -> (row_ind, col_ind, status) as linear_sum_assignment_batched; status 4:
+    a problem outside the candidate-list class (cube_free_scenes)."""
+    if not plan.resid:
+        raise ValueError("linear_sum_assignment_resid needs LsapPlan(..., resid=True)")
+    dev = bmin8.device
+    row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
+    col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
+    status = torch.empty(plan.n, dtype=torch.int32, device=dev)
+    torch.ops.mvmatch.lsap_solve_resid_out(plan.dims, plan.ws_offs, plan.out_offs, plan.workspace,
+                                           row_ind, col_ind, status, bmin8, tplan.bmin8_offs,
+                                           tplan.segs, tplan.workspace, tplan.max_n, plan.long_min,
+                                           plan.long_max, plan.short_max, _opts_list(options))
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
 
 
@@ -666,4 +827,22 @@ def select_triangulate(cube: Tensor, cube_offs: Tensor, cam_offs: Tensor, lsap_o
     torch.ops.mvmatch.select_triangulate_out(cube, cube_offs, cam_offs, lsap_offs, row_ind,
                                              col_ind, pts, proj.contiguous(), float(threshold),
                                              match, cost, X, count)
+    return match, cost, X, count
+
+
+def select_triangulate_resid(tplan: TripletPlan, cam_offs: Tensor, lsap_offs: Tensor,
+                             row_ind: Tensor, col_ind: Tensor, pts: Tensor, proj: Tensor,
+                             threshold: float):
+    """select_triangulate for a ``triplet_minima(..., tplan)`` batch: each
+    assigned entry recomputed from the residuals in ``tplan.workspace``."""
+    dev = pts.device
+    cap = int(row_ind.numel())
+    n_scenes = int(lsap_offs.numel()) - 1
+    match = torch.empty((cap, 3), dtype=torch.int32, device=dev)
+    cost = torch.empty(cap, dtype=torch.float32, device=dev)
+    X = torch.empty((cap, 3), dtype=torch.float64, device=dev)
+    count = torch.empty(n_scenes, dtype=torch.int32, device=dev)
+    torch.ops.mvmatch.select_triangulate_resid_out(tplan.workspace, tplan.max_n, cam_offs, lsap_offs,
+                                                   row_ind, col_ind, pts, proj.contiguous(),
+                                                   float(threshold), match, cost, X, count)
     return match, cost, X, count

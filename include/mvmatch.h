@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MVM_ABI_VERSION 6
+#define MVM_ABI_VERSION 7
 #define MVM_MAX_CAMS 8
 #define MVM_MAX_PAIRS 28 /* MVM_MAX_CAMS choose 2 */
 
@@ -268,6 +268,27 @@ int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs
                                   const mvm_options *opts, mvm_stream_t stream);
 
 /*
+ * Cube-free association input (ABI 7): for an assignment of every scene's
+ * flattened (N*M, P) cube that never reads the cube itself
+ * (mvm_lsap_solve_resid, mvm_select_triangulate_resid), write only what
+ * those need -- the same 16-bit 8-row minima mvm_triplet_cost_argmin_bmin8
+ * writes (bit for bit, same layout and offsets) and every scene's float64 pair
+ * residuals, from which they recompute the entries they read as
+ * float32(((e12 + e13) + e23) / 3), the cube's own arithmetic:
+ *   resid_dev + s * stride             e12  [N][ld]  (i, j)
+ *   resid_dev + s * stride + max_n*ld  e13T [P][ld]  (k, i)   (transposed)
+ *   resid_dev + s * stride + 2*max_n*ld e23T [P][ld] (k, j)   (transposed)
+ * with ld = roundup(max_n, 4), stride = 3 * max_n * ld; resid_bytes >=
+ * mvm_triplet_workspace_bytes(n_scenes, max_n) (16-byte aligned).  Views of at
+ * most 256 detections.  Replaces the cube's 4 B per triple of HBM writes with
+ * ~2 B per 8 triples (epipolar_matching.py:83-98 feeding :100-116).
+ */
+int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
+                       int32_t n_scenes, int32_t max_n, uint16_t *bmin8_dev,
+                       const int64_t *bmin8_offs_dev, double *resid_dev, size_t resid_bytes,
+                       const mvm_options *opts, mvm_stream_t stream);
+
+/*
  * Batched rectangular linear-sum assignment, identical to
  * scipy.optimize.linear_sum_assignment (the association step of
  * match_objects, bpc/inference/epipolar_matching.py:100-116, scipy 1.14's
@@ -341,6 +362,39 @@ int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *
                        const int64_t *segs_dev, const mvm_options *opts, mvm_stream_t stream);
 
 /*
+ * Cube-free assignment (ABI 7): mvm_lsap_solve_ex3 for the flattened (N*M, P)
+ * cubes of a mvm_triplet_minima batch, without the cubes.  Problem p is
+ * scene p: dims (N*M, P), segs_dev[p] = M, its 8-row minima at bmin8_dev +
+ * bmin8_offs_dev[p] and its pair residuals at resid_dev (max_n as given to
+ * mvm_triplet_minima); the kernels recompute every entry they read with the
+ * cube's arithmetic, so the result is that of mvm_lsap_solve_ex3 on the cubes
+ * (and scipy's).  There is no cost for the dense classes to read, so every
+ * non-empty problem must be of the candidate-list class (long sides >=
+ * mvm_options.lsap_sparse_min_cols (default 4096) and > lsap_wave_max_cols
+ * (1024), <= 65536; short sides <= 1024): the host bounds are checked
+ * (MVM_ERR_INVALID_ARGUMENT), and a problem outside them on the device gets
+ * status 4.  The workspace comes from mvm_lsap_plan_resid (the class's
+ * candidate lists only: ~0.3 MB per 256^3 scene).
+ * Statuses of every mvm_lsap_solve* entry point: 0 ok, 1 NaN / -inf entries
+ * (scipy's ValueError), 2 infeasible, 3 internal (a co-resident wait timed
+ * out), 4 the problem exceeds the bounds the call was given (short_max /
+ * long_max) or, here, is outside the class.
+ */
+int64_t mvm_lsap_plan_resid(int32_t n_problems, const int64_t *rows, const int64_t *cols,
+                            int64_t *ws_offs, int64_t *out_offs);
+/* The candidate-list class's limits (ABI 7): the default lower bound of its
+ * long sides (mvm_options.lsap_sparse_min_cols 0), its largest long side and
+ * its largest short side.  Any pointer may be NULL. */
+void mvm_lsap_sparse_bounds(int32_t *min_cols, int32_t *max_cols, int32_t *max_short);
+int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
+                         const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
+                         int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
+                         int64_t long_min, int64_t long_max, int64_t short_max,
+                         const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                         const int64_t *segs_dev, const double *resid_dev, int32_t max_n,
+                         const mvm_options *opts, mvm_stream_t stream);
+
+/*
  * On-device detection packing, replacing the per-box loop of
  * PoseEstimator._detect (bpc/inference/process_pose.py:122-140).  Input:
  * the detector's boxes of n_img images in CSR form: boxes_dev f32 [n, 4]
@@ -394,6 +448,15 @@ int mvm_select_triangulate(const float *cube_dev, const int64_t *cube_offs_dev,
                            const double *pts_dev, const double *proj_dev, int32_t n_scenes,
                            double threshold, int32_t *match_dev, float *cost_dev, double *X_dev,
                            int32_t *count_dev, mvm_stream_t stream);
+/* ... cube-free (ABI 7): each assigned entry recomputed from the pair
+ * residuals of mvm_triplet_minima (resid_dev, max_n as given there) with the
+ * cube's arithmetic -- the same costs, matches and order as from the cube. */
+int mvm_select_triangulate_resid(const double *resid_dev, int32_t max_n, const int64_t *cam_offs_dev,
+                                 const int64_t *lsap_out_offs_dev, const int64_t *row_ind_dev,
+                                 const int64_t *col_ind_dev, const double *pts_dev,
+                                 const double *proj_dev, int32_t n_scenes, double threshold,
+                                 int32_t *match_dev, float *cost_dev, double *X_dev, int32_t *count_dev,
+                                 mvm_stream_t stream);
 
 /*
  * Diagnostic: fill `bytes` (multiple of 16, 16-byte aligned) of device memory

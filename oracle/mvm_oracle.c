@@ -230,6 +230,47 @@ void mvm_oracle_cube(const double *pts, const int64_t *cam_offs, const double *F
 }
 
 /* OpenMP thread count the baseline will use. */
+/* The fp64 pair residuals of every 3-camera scene (pairs (0,1), (0,2), (1,2):
+ * epipolar_matching.py:78-80) in the layout of the GPU's cube-free path
+ * (include/mvmatch.h, mvm_triplet_minima): e12 [N][ld], then e13 and e23
+ * TRANSPOSED, [P][ld] each, at out + s * 3 * max_n * ld.  Entries outside the
+ * views are left untouched. */
+void mvm_oracle_residuals(const double *pts, const int64_t *cam_offs, const double *F, int S,
+                          int max_n, int64_t ld, double *out, int nthreads) {
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#else
+    (void)nthreads;
+#endif
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int s = 0; s < S; ++s) {
+        int64_t o1 = cam_offs[3 * s], N = cam_offs[3 * s + 1] - o1;
+        int64_t o2 = cam_offs[3 * s + 1], M = cam_offs[3 * s + 2] - o2;
+        int64_t o3 = cam_offs[3 * s + 2], Pn = cam_offs[3 * s + 3] - o3;
+        const double *F12 = F + (int64_t)s * 27, *F13 = F12 + 9, *F23 = F12 + 18;
+        int64_t mx = M > Pn ? M : Pn;
+        line_t *lc = (line_t *)malloc(sizeof(line_t) * (size_t)(mx > 0 ? mx : 1));
+        double *e13 = (double *)malloc(sizeof(double) * (size_t)(N * Pn + 1));
+        double *e23 = (double *)malloc(sizeof(double) * (size_t)(M * Pn + 1));
+        double *E12 = out + (int64_t)s * 3 * max_n * ld, *E13T = E12 + (int64_t)max_n * ld,
+               *E23T = E13T + (int64_t)max_n * ld;
+        double *e12 = (double *)malloc(sizeof(double) * (size_t)(N * M + 1));
+        residual_matrix_f64(F12, pts, o1, N, o2, M, lc, e12);
+        residual_matrix_f64(F13, pts, o1, N, o3, Pn, lc, e13);
+        residual_matrix_f64(F23, pts, o2, M, o3, Pn, lc, e23);
+        for (int64_t i = 0; i < N; ++i)
+            for (int64_t j = 0; j < M; ++j) E12[i * ld + j] = e12[i * M + j];
+        for (int64_t k = 0; k < Pn; ++k) {
+            for (int64_t i = 0; i < N; ++i) E13T[k * ld + i] = e13[i * Pn + k];
+            for (int64_t j = 0; j < M; ++j) E23T[k * ld + j] = e23[j * Pn + k];
+        }
+        free(lc);
+        free(e12);
+        free(e13);
+        free(e23);
+    }
+}
+
 int mvm_oracle_max_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -42,6 +42,8 @@ def lib():
         L.mvm_oracle_pairwise.argtypes = [vp, vp, vp, vp, i, i, i, vp, vp, vp, vp, vp, i]
         L.mvm_oracle_cube.restype = None
         L.mvm_oracle_cube.argtypes = [vp, vp, vp, i, vp, vp, vp, vp, vp, i]
+        L.mvm_oracle_residuals.restype = None
+        L.mvm_oracle_residuals.argtypes = [vp, vp, vp, i, i, ctypes.c_int64, vp, i]
         L.mvm_oracle_max_threads.restype = i
         _lib = L
     return _lib
@@ -119,3 +121,31 @@ def cube(pts, cam_offs, F, n_scenes, *, want_cube=True, nthreads: int = 0):
 
 def max_threads() -> int:
     return int(lib().mvm_oracle_max_threads())
+
+
+def residuals(pts, cam_offs, F, n_scenes: int, max_n: int, *, nthreads: int = 0) -> np.ndarray:
+    """fp64 pair residuals of every 3-camera scene in the GPU cube-free layout
+    (mvm_triplet_minima): f64 [S, 3, max_n, ld] = e12 [N][ld], e13T [P][ld],
+    e23T [P][ld]; entries outside the views are NaN."""
+    pts = np.ascontiguousarray(pts, np.float64)
+    cam_offs = np.ascontiguousarray(cam_offs, np.int64)
+    F = np.ascontiguousarray(F, np.float64)
+    ld = (max_n + 3) // 4 * 4
+    out = np.full((n_scenes, 3, max_n, ld), np.nan)
+    lib().mvm_oracle_residuals(_ptr(pts), _ptr(cam_offs), _ptr(F), n_scenes, max_n, ld, _ptr(out),
+                               nthreads)
+    return out
+
+
+def bmin8_keys(cube: np.ndarray) -> np.ndarray:
+    """The 16-bit 8-row minima of one (N, M, P) float32 cube, as
+    mvm_triplet_cost_argmin_bmin8 / mvm_triplet_minima write them: per (i,
+    group of 8 j, k) the upper half of (bits | 0x80000000) of the group's
+    minimum, 0 when any of the group is NaN -> uint16 [N, ceil(M/8), P]."""
+    N, M, P = cube.shape
+    g8 = (M + 7) // 8
+    pad = np.full((N, g8 * 8, P), np.inf, np.float32)
+    pad[:, :M] = cube
+    key = pad.view(np.uint32) | np.uint32(0x80000000)
+    key = np.where(np.isnan(pad), np.uint32(0), key)
+    return (key.reshape(N, g8, 8, P).min(axis=2) >> 16).astype(np.uint16)

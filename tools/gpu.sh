@@ -25,6 +25,8 @@
 #   bash tools/gpu.sh bm8ab                   the 8-row-minima and assignment suites, then
 #                                             the assignment's block-minima source by view
 #                                             size (tools/ab_bmin8_input.py)
+#   bash tools/gpu.sh cubefree [bench args]  the cube-free association's suites, the
+#                                             c2match line without / with the cube, its trace
 #   AB_LIBS="a.so b.so" bash tools/gpu.sh ab CMD...
 #                                             in-tree library builds (MVM_LIB_PATH) timed by
 #                                             CMD in alternating processes, AB_ROUNDS rounds
@@ -146,6 +148,22 @@ bm8ab)
       > "$O/bm8ab_${spec#*:}.log" 2>&1 || fail "bm8ab $spec" "$O/bm8ab_${spec#*:}.log"
     grep -E "minima|itself" "$O/bm8ab_${spec#*:}.log"
   done ;;
+cubefree)
+  # the cube-free association (ABI 7): its suite and the assignment / pipeline
+  # suites, then the c2match line without and with the cube, and its trace
+  timeout -k 10 900 python -u -m pytest tests/test_cubefree_gpu.py tests/test_lsap_bmin8_gpu.py \
+    tests/test_lsap_gpu.py tests/test_batch_match_gpu.py -x -q --timeout 240 --timeout-method thread \
+    > "$O/pytest_cubefree.log" 2>&1 || fail "cube-free suites" "$O/pytest_cubefree.log"
+  tail -1 "$O/pytest_cubefree.log"
+  for M in free keep free keep; do
+    timeout -k 10 "$LIMIT" python -u bench.py --workload c2match --cube $M --cpu-seconds 0 "$@" \
+      >> "$O/bench_c2match_$M.json" 2>> "$O/bench_c2match_$M.err" || fail "c2match $M" "$O/bench_c2match_$M.err"
+    python tools/summarise_line.py <(tail -1 "$O/bench_c2match_$M.json")
+  done
+  timeout -k 10 "$LIMIT" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace_c2match_free" \
+    -o run -- python -u bench.py --workload c2match --cube free --cpu-seconds 0 "$@" \
+    > "$O/trace_c2match_free.json" 2> "$O/trace_c2match_free.err"
+  rc=$?; echo "cubefree trace rc=$rc"; exit $rc ;;
 ab)
   for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
     for lib in $AB_LIBS; do

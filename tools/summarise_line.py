@@ -13,3 +13,12 @@ print(f"{d['config'].get('launch_mode')} N={d['n_gpus']} value {d['value']:.4g} 
       f"sclk {d['sclk'].get('mean_mhz', 0):.0f} cpu {cpu.get('value', 0):.3g} "
       f"tail {sp.get('exposed_tail_ms', 0):.3f} ms | {d['parity']} | rows: {d.get('parity_rows')}"
       + (f" | slots fastest/slowest {r['per_slot']['fastest_over_slowest']:.3f}" if r.get('per_slot') else ""))
+st = d.get("stages_ms")
+if st:
+    print("  stages ms: " + ", ".join(f"{k} {v:.3f}" for k, v in st.items() if k != "note")
+          + f" | valu {((d.get('valu_roofline') or {}).get('frac') or 0):.3f}")
+n = d.get("c2match")
+if n:
+    print(f"  c2match: {n['value']:.4g} {n['unit']} ms/step {n['ms_per_step']:.3f} | "
+          + ", ".join(f"{k} {v:.3f}" for k, v in n["stages_ms"].items() if k != "note")
+          + f" | {n['parity']} | wall {n.get('wall_s', 0):.1f} s")
