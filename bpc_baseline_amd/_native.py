@@ -142,6 +142,7 @@ SIGNATURES = {
         _vp, _vp, _vp, _vp, _vp]),          # bmin8, bmin8_offs, segs, options, stream
     "mvm_lsap_plan_resid": (_i64, [_i32, _vp, _vp, _vp, _vp]),
     "mvm_lsap_sparse_bounds": (None, [_vp, _vp, _vp]),
+    "mvm_lsap_sparse_stats_offset": (_i64, [_i64, _i64]),
     "mvm_lsap_solve_resid": (ctypes.c_int, [
         _vp, _i32, _vp, _vp,                # dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp,            # workspace, bytes, row_ind, col_ind, status

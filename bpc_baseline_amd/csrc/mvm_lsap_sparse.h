@@ -73,8 +73,13 @@ __host__ __device__ inline bool lsap_sparse_class(int32_t lo, int32_t wave_max, 
 
 // per-problem workspace of the class (inside the plan's region for the problem)
 struct SpLayout {
-    size_t flags, bm, lcol, lval, ln, theta, total;
+    size_t stats, flags, bm, lcol, lval, ln, theta, total;
 };
+// sp_solve_kernel's counters of a solved problem, int32 at the start of its
+// workspace region (mvm_lsap_sparse_stats reads them): dense scans for a row's
+// free minimum (no list, or no free entry left in it), dense scans for the
+// free ties at the sink, rows whose list overflowed kSpLCap, Dijkstra steps
+constexpr int kSpStats = 4;
 
 // tr: the problem is tall (transposed, short side = columns)
 __host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, size_t elem, bool tr) {
@@ -92,6 +97,7 @@ __host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, siz
     const int64_t nbf = (L + kSpBlock - 1) / kSpBlock, nbs = L < kSpMaxBlocks ? L : kSpMaxBlocks;
     const int64_t nb = tr && nbs > nbf ? nbs : nbf;
     const int64_t nt = (L + kSpTileCols - 1) / kSpTileCols;
+    y.stats = take(kSpStats * 4);
     y.flags = take((size_t)(nt > 32 ? nt : 32) * 4);   // invalid-entry flag per tile
     y.bm = take((size_t)S * nb * elem);              // ordered keys of the block minima
     y.lcol = take((size_t)S * kSpLCap * 4);

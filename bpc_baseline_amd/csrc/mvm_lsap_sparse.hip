@@ -703,13 +703,23 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
             return;
         }
     }
+    // statistics (kSpStats): rows whose list overflowed, then per search
+    __shared__ int s_novf;
+    if (t == 0) s_novf = 0;
+    int n_dense_min = 0, n_dense_tie = 0, n_steps = 0;   // thread 0's (uniform) counts
     for (int x = t; x < lw; x += kSpNT) {
         s_asg[x] = 0u;
         s_mvb[x] = 0u;
     }
-    for (int x = t; x < S; x += kSpNT) {
-        s_u[x] = 0.0;
-        s_c4r[x] = -1;
+    __syncthreads();
+    {
+        int ovf = 0;
+        for (int x = t; x < S; x += kSpNT) {
+            s_u[x] = 0.0;
+            s_c4r[x] = -1;
+            ovf += ln[x] < 0;
+        }
+        if (ovf) atomicAdd(&s_novf, ovf);
     }
     // slot state: slot q = t + 256 m lives in thread t's registers
     double v[KS], spc[KS];
@@ -816,6 +826,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
             double rb;
             if (nl < 0 || !f_any) {
                 // no free list entry (or no list): the row's free minimum densely
+                ++n_dense_min;
                 double d = INFINITY;
                 for (int j0 = t; j0 < L; j0 += kSpNT * 8) {
                     CT c[8];
@@ -855,6 +866,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                     const double mp = s_mp[s], us = s_u[is], rbs = s_rb[s];
                     const int nls = ln[is];
                     const bool dense = nls < 0 || rbs != rbs || rbs == lowest;
+                    n_dense_tie += dense;
                     long long key = -1;
                     if (!dense) {
                         if (t < nls) {
@@ -947,6 +959,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                 return;
             }
         }
+        n_steps += k + 1;
         if (sink < 0) {                                       // infeasible: scipy's ValueError
             if (t == 0) a.status[p] = 2;
             return;
@@ -980,6 +993,13 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
             }
         }
         __syncthreads();
+    }
+    if (t == 0) {
+        int32_t *stt = reinterpret_cast<int32_t *>(a.ws + a.ws_offs[p] + y.stats);
+        stt[0] = n_dense_min;
+        stt[1] = n_dense_tie;
+        stt[2] = s_novf;
+        stt[3] = n_steps;
     }
     // ---- output in scipy's order
     const int64_t o = a.out_offs[p];
@@ -1047,6 +1067,11 @@ int lsap_sparse_launch_f64(const LsapSparseArgs &a, int32_t n, int64_t long_max,
 
 // ================================================================ C ABI ====
 extern "C" {
+
+int64_t mvm_lsap_sparse_stats_offset(int64_t rows, int64_t cols) {
+    const bool tr = cols < rows;
+    return (int64_t)lsap_sparse_layout(tr ? cols : rows, tr ? rows : cols, sizeof(float), tr).stats;
+}
 
 void mvm_lsap_sparse_bounds(int32_t *min_cols, int32_t *max_cols, int32_t *max_short) {
     if (min_cols) *min_cols = kSparseMinCols;

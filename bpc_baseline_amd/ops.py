@@ -36,7 +36,7 @@ __all__ = [
     "hbm_write_probe", "LsapPlan", "linear_sum_assignment_batched",
     "pack_detections", "triangulate_dlt", "select_triangulate",
     "triplet_minima", "linear_sum_assignment_resid", "select_triangulate_resid",
-    "cube_free_scenes", "sparse_class_bounds",
+    "cube_free_scenes", "sparse_class_bounds", "lsap_sparse_stats",
 ]
 
 
@@ -714,6 +714,7 @@ class LsapPlan:
         if total < 0:
             raise _native.MvmError(fn, -1, _native.load().mvm_last_error_string().decode())
         self.resid = bool(resid)
+        self.ws_offs_host = ws_offs
         self.dtype = dtype
         self.n = n
         self.rows, self.cols = rows, cols
@@ -755,6 +756,29 @@ def linear_sum_assignment_batched(cost: Tensor, cost_offs: Tensor, plan: LsapPla
                                      plan.workspace, row_ind, col_ind, status, plan.long_min,
                                      plan.long_max, _opts_list(options), plan.short_max)
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
+
+
+def lsap_sparse_stats(plan: LsapPlan, min_cols: Optional[int] = None) -> np.ndarray:
+    """After a solve with ``plan``: per problem the candidate-list solver's
+    counters (mvm_lsap_sparse_stats_offset) -- int64 [n, 4] = dense free-minimum
+    scans, dense tie scans, overflowed lists, Dijkstra steps; -1 for problems
+    outside the class (``min_cols``: its lower bound if not the default)."""
+    lib = _native.load()
+    lo, hi, sh = sparse_class_bounds()
+    lo = lo if min_cols is None else int(min_cols)
+    lng, sht = np.maximum(plan.rows, plan.cols), np.minimum(plan.rows, plan.cols)
+    cls = (lng >= lo) & (lng > 1024) & (lng <= hi) & (sht >= 1) & (sht <= sh)
+    out = np.full((plan.n, 4), -1, np.int64)
+    if not cls.any():
+        return out
+    ps = np.nonzero(cls)[0]
+    offs = np.array([plan.ws_offs_host[p] + lib.mvm_lsap_sparse_stats_offset(int(plan.rows[p]),
+                                                                             int(plan.cols[p]))
+                     for p in ps], np.int64)
+    idx = torch.from_numpy((offs[:, None] // 4 + np.arange(4)).reshape(-1)).to(plan.workspace.device)
+    words = plan.workspace[:plan.workspace.numel() // 4 * 4].view(torch.int32)
+    out[ps] = words.index_select(0, idx).cpu().numpy().reshape(-1, 4)
+    return out
 
 
 def linear_sum_assignment_resid(plan: LsapPlan, tplan: TripletPlan, bmin8: Tensor, *,

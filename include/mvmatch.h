@@ -386,6 +386,12 @@ int64_t mvm_lsap_plan_resid(int32_t n_problems, const int64_t *rows, const int64
  * long sides (mvm_options.lsap_sparse_min_cols 0), its largest long side and
  * its largest short side.  Any pointer may be NULL. */
 void mvm_lsap_sparse_bounds(int32_t *min_cols, int32_t *max_cols, int32_t *max_short);
+/* Byte offset, inside a (rows x cols) problem's workspace region, of the
+ * candidate-list solver's counters for it (ABI 7): int32 [4] = dense scans for
+ * a row's free minimum (no list, or no free entry left in it), dense scans for
+ * the free ties at a search's end, rows whose candidate list overflowed,
+ * Dijkstra steps.  Written by every solve of a problem of that class. */
+int64_t mvm_lsap_sparse_stats_offset(int64_t rows, int64_t cols);
 int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int64_t *ws_offs_dev,
                          const int64_t *out_offs_dev, void *workspace_dev, size_t workspace_bytes,
                          int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,

@@ -204,3 +204,73 @@ def test_lsap_plan_dtype(lib):
     assert t64 - t32 >= 300 * 20 * 4
     assert lib.mvm_lsap_plan_ex(2, rows.ctypes.data, cols.ctypes.data, 7, w32.ctypes.data,
                                 o.ctypes.data) == -1
+
+
+# ---- the cube-free association (ABI 7) ----------------------------------------
+def test_cube_free_class_bounds_and_scenes(lib):
+    import numpy as np
+    from bpc_baseline_amd import ops
+    assert ops.sparse_class_bounds() == (4096, 65536, 1024)
+    counts = np.array([[256, 256, 256],    # 65536 x 256: the class
+                       [64, 64, 64],       # 4096 x 64: its lower edge
+                       [63, 64, 64],       # 4032: below it (the dense classes read a cube)
+                       [0, 100, 100],      # empty: nothing to read
+                       [100, 100, 0],
+                       [300, 20, 40],      # a view of more than 256: no minima kernel
+                       [256, 256, 1]])     # one column
+    assert ops.cube_free_scenes(counts).tolist() == [True, True, False, True, True, False, True]
+    assert ops.cube_free_scenes(counts, min_cols=2048).tolist() == [True, True, True, True, True,
+                                                                     False, True]
+
+
+def test_lsap_plan_resid_sizes(lib):
+    import numpy as np
+    rows = np.array([65536, 4096, 600, 0, 24], np.int64)
+    cols = np.array([256, 64, 40, 10, 576], np.int64)
+    ws = np.zeros(6, np.int64)
+    out = np.zeros(6, np.int64)
+    total = lib.mvm_lsap_plan_resid(5, rows.ctypes.data, cols.ctypes.data, ws.ctypes.data, out.ctypes.data)
+    assert total == ws[-1] > 0
+    assert out.tolist() == [0, 256, 320, 360, 360, 384]
+    sizes = np.diff(ws)
+    assert sizes[3] == 0                              # an empty problem reserves nothing
+    # a 256^3 scene: its candidate lists and block minima, no transposed cost
+    assert 2e6 < sizes[0] < 3e6
+    # the dense plan reserves the transposed cost for the same problem
+    ws2 = np.zeros(6, np.int64)
+    lib.mvm_lsap_plan_ex(5, rows.ctypes.data, cols.ctypes.data, 0, ws2.ctypes.data, out.ctypes.data)
+    assert np.diff(ws2)[0] > 60e6
+    # a wide problem reserves ceil(L/32) block keys per row, not L
+    assert sizes[4] < 24 * 576 * 4
+    assert lib.mvm_lsap_plan_resid(-1, None, None, None, None) == -1
+    assert lib.mvm_lsap_sparse_stats_offset(65536, 256) == 0
+
+
+def test_lsap_solve_resid_validation(lib):
+    """Host bounds that are not all of the candidate-list class are refused
+    before anything is launched (there is no cost for another class to read)."""
+    def call(long_min, long_max, short_max, max_n=256, n=3):
+        return lib.mvm_lsap_solve_resid(FAKE, n, FAKE, FAKE, FAKE, 1 << 20, FAKE, FAKE, FAKE,
+                                        long_min, long_max, short_max, FAKE, FAKE, FAKE, FAKE, max_n,
+                                        None, None)
+    assert call(600, 65536, 256) == 1
+    assert b"candidate-list class" in lib.mvm_last_error_string()
+    assert call(4096, 70000, 256) == 1
+    assert call(4096, 65536, 2000) == 1
+    assert call(4096, 65536, 256, max_n=300) == 2          # views of more than 256
+    assert call(4096, 65536, 256, n=0) == 0                # nothing to solve
+    assert lib.mvm_lsap_solve_resid(None, 3, FAKE, FAKE, FAKE, 0, FAKE, FAKE, FAKE, 4096, 65536, 256,
+                                    FAKE, FAKE, FAKE, FAKE, 256, None, None) == 1
+
+
+def test_triplet_minima_validation(lib):
+    need = lib.mvm_triplet_workspace_bytes(10, 200)
+    args = lambda max_n, nbytes, resid=FAKE: (FAKE, FAKE, FAKE, 10, max_n, FAKE, FAKE, resid, nbytes,
+                                              None, None)
+    assert lib.mvm_triplet_minima(*args(300, 1 << 40)) == 2          # views of more than 256
+    assert lib.mvm_triplet_minima(*args(200, need - 8)) == 3         # workspace too small
+    assert lib.mvm_triplet_minima(*args(200, need, ctypes.c_void_p(0x1008))) == 1   # misaligned
+    assert lib.mvm_triplet_minima(*args(200, need, None)) == 1       # null pointer
+    assert lib.mvm_triplet_minima(None, None, None, 0, 0, None, None, None, 0, None, None) == 0
+    assert lib.mvm_select_triangulate_resid(None, 10, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, 3, 30.0,
+                                            FAKE, FAKE, FAKE, FAKE, None) == 1
