@@ -724,11 +724,18 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
     // slot state: slot q = t + 256 m lives in thread t's registers
     double v[KS], spc[KS];
     int32_t col[KS], pos[KS], ps[KS];
+    // cube-free: the slot's column as cube (i, j) and its e12, set when the
+    // column is assigned (a slot keeps its column), so a step gathers only the
+    // visited row's e13T / e23T entries
+    int32_t sic[KS], sjc[KS];
+    double se12[KS];
     uint32_t rem = 0;                                         // bit m: slot removed this search
 #pragma unroll
     for (int m = 0; m < KS; ++m) {
         v[m] = 0.0;
         col[m] = -1;
+        sic[m] = sjc[m] = 0;
+        se12[m] = 0.0;
     }
     __syncthreads();
     auto asg = [&](int j) { return (s_asg[j >> 5] >> (j & 31)) & 1u; };
@@ -757,7 +764,13 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
 #pragma unroll
             for (int m = 0; m < KS; ++m) {
                 const int q = t + kSpNT * m;
-                cv[m] = (q < na && !((rem >> m) & 1u)) ? src.at(i, col[m]) : (CT)0;
+                const bool live = q < na && !((rem >> m) & 1u);
+                if (src.e12)
+                    cv[m] = live ? (CT)cube_f32(se12[m], src.e13t[i * src.ld + sic[m]],
+                                                src.e23t[i * src.ld + sjc[m]])
+                                 : (CT)0;
+                else
+                    cv[m] = live ? src.at(i, col[m]) : (CT)0;
             }
             int lc = 0;
             CT lv = (CT)0;
@@ -973,6 +986,12 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
             if (t + kSpNT * m == na) {                       // slot na: the sink, v stays 0
                 col[m] = sink;
                 v[m] = 0.0;
+                if (src.e12) {
+                    int jj;
+                    sic[m] = sp_div(sink, src.M, src.rM, jj);
+                    sjc[m] = jj;
+                    se12[m] = src.e12[sic[m] * src.ld + jj];
+                }
             }
         }
         for (int mm = t; mm < n_mv; mm += kSpNT) {
