@@ -1518,7 +1518,7 @@ struct MinimaArgs {
 };
 
 template <int IB>
-__global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs args) {
+__global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_kernel(MinimaArgs args) {
     constexpr int RPW = 8;                     // j rows per wave: one 8-row group
     constexpr int kJ = kWaves * RPW;           // j per workgroup
     struct ColRec {
@@ -1652,6 +1652,7 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     for (int i0 = 0; i0 < N; i0 += IB) {
         const int ni = min(IB, N - i0);
         bool deg_rows = false;
+        static_assert(IB <= kWave, "the chunk's row lines: one thread of wave 0 each");
         if (t < IB) {
             LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
             double px = 0.0, py = 0.0;
@@ -1870,10 +1871,17 @@ int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const
     a.max_n = max_n;
     a.stride = (int64_t)3 * max_n * a.ld;
     a.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
+    if (o.cube_tile_rows != 0 && o.cube_tile_rows != 16 && o.cube_tile_rows != 32)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_tile_rows %d not 0, 16 or 32", (int)o.cube_tile_rows);
     const int64_t blocks = (int64_t)n_scenes * a.j_blocks;
     if ((st = grid_check(blocks))) return st;
-    triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0,
-                                reinterpret_cast<hipStream_t>(stream)>>>(a);
+    const hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
+    // i rows per chunk (mvm_options.cube_tile_rows): 16 by default (four
+    // workgroups per CU), 32 halves the per-chunk barriers and row lines (two)
+    if (o.cube_tile_rows == 32)
+        triplet_minima_kernel<32><<<dim3((unsigned)blocks), dim3(kThreads), 0, hs>>>(a);
+    else
+        triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0, hs>>>(a);
     return mvm_check_launch("triplet_minima_kernel");
 }
 

@@ -37,7 +37,7 @@ def _scenes(counts, seed, nan_scene=None, nan_view=2, degenerate_scene=None):
     return pts, F, co
 
 
-def _minima(cuda, counts, seed, **kw):
+def _minima(cuda, counts, seed, options=None, **kw):
     from bpc_baseline_amd import ops
     pts, F, co = _scenes(counts, seed, **kw)
     plan = ops.TripletPlan(co, len(counts), device=cuda)
@@ -45,7 +45,7 @@ def _minima(cuda, counts, seed, **kw):
     P, C, FF = t(pts), t(co), t(F)
     bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int16, device=cuda)
     plan.workspace.fill_(0xFF)                       # NaN everywhere the kernel does not write
-    ops.triplet_minima(P, C, FF, plan, bmin8=bm8)
+    ops.triplet_minima(P, C, FF, plan, bmin8=bm8, options=options)
     return plan, bm8, (pts, F, co), (P, C, FF)
 
 
@@ -58,11 +58,14 @@ MINIMA_BATCHES = {
 
 
 @pytest.mark.parametrize("batch", sorted(MINIMA_BATCHES))
-def test_minima_equal_cube_kernel_and_oracle(cuda, batch):
+@pytest.mark.parametrize("rows", [0, 32])
+def test_minima_equal_cube_kernel_and_oracle(cuda, batch, rows):
+    """rows: i rows per chunk (mvm_options.cube_tile_rows; 0 = 16)"""
     from bpc_baseline_amd import ops
     from oracle import oracle as O
     counts = MINIMA_BATCHES[batch]
-    plan, bm8, (pts, F, co), (P, C, FF) = _minima(cuda, counts, 5)
+    plan, bm8, (pts, F, co), (P, C, FF) = _minima(cuda, counts, 5,
+                                                  options={"cube_tile_rows": rows} if rows else None)
     got = bm8.cpu().numpy().view(np.uint16)
     # the cube kernel's own minima on the same batch
     ref8 = torch.full_like(bm8, -1)
@@ -86,14 +89,16 @@ def test_minima_equal_cube_kernel_and_oracle(cuda, batch):
             assert np.array_equal(g.view(np.int64), w.view(np.int64)), (batch, s, m)
 
 
-def test_minima_nonfinite_chunks(cuda):
+@pytest.mark.parametrize("rows", [0, 32])
+def test_minima_nonfinite_chunks(cuda, rows):
     """NaN centroids and a degenerate F: the chunks with non-finite or huge
     residuals take the exact per-entry path (keys equal the oracle's)."""
     from oracle import oracle as O
     counts = [(40, 70, 50), (64, 64, 64), (30, 100, 17)]
+    opts = {"cube_tile_rows": rows} if rows else None
     for kw in ({"nan_scene": 1, "nan_view": 0}, {"nan_scene": 0, "nan_view": 1},
                {"nan_scene": 2, "nan_view": 2}, {"degenerate_scene": 1}):
-        plan, bm8, (pts, F, co), _ = _minima(cuda, counts, 9, **kw)
+        plan, bm8, (pts, F, co), _ = _minima(cuda, counts, 9, options=opts, **kw)
         got = bm8.cpu().numpy().view(np.uint16)
         oc = O.cube(pts, co, F, len(counts))[0]
         for s, (N, M, Pn) in enumerate(counts):

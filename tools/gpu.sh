@@ -164,6 +164,33 @@ cubefree)
     -o run -- python -u bench.py --workload c2match --cube free --cpu-seconds 0 "$@" \
     > "$O/trace_c2match_free.json" 2> "$O/trace_c2match_free.err"
   rc=$?; echo "cubefree trace rc=$rc"; exit $rc ;;
+cfab)
+  # the cube-free chain's options A/B on the c2match line (alternating), then
+  # one SQ counter pass over it
+  timeout -k 10 600 python -u -m pytest tests/test_cubefree_gpu.py -x -q --timeout 240 \
+    --timeout-method thread > "$O/pytest_cfab.log" 2>&1 || fail "cube-free suite" "$O/pytest_cfab.log"
+  tail -1 "$O/pytest_cfab.log"
+  for rnd in 1 2; do
+    for V in ${CF_VARIANTS:-default cube_tile_rows=32}; do
+      OPT=""; [ "$V" != default ] && OPT="--options $V"
+      timeout -k 10 "$LIMIT" python -u bench.py --workload c2match --cube free --cpu-seconds 0 $OPT "$@" \
+        > "$O/cf_${V}_$rnd.json" 2> "$O/cf_${V}_$rnd.err" || fail "c2match $V" "$O/cf_${V}_$rnd.err"
+      echo "== $V round $rnd"; python tools/summarise_line.py "$O/cf_${V}_$rnd.json" | tail -1
+    done
+  done
+  for C in ${CF_CHUNKS:-2 4}; do
+    timeout -k 10 "$LIMIT" python -u bench.py --workload c2match --cube free --cpu-seconds 0 --match-chunks $C "$@" \
+      > "$O/cf_chunks$C.json" 2> "$O/cf_chunks$C.err" || fail "c2match chunks $C" "$O/cf_chunks$C.err"
+    echo "== $C chunks"; python tools/summarise_line.py "$O/cf_chunks$C.json"
+  done
+  timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY \
+    SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_LDS --output-format csv -d "$O/sq_cf" -o run -- \
+    python bench.py --workload c2match --cube free --steps 2 --warmup 1 --cpu-seconds 0 > "$O/sq_cf.log" 2>&1 \
+    || fail "sq c2match" "$O/sq_cf.log"
+  for K in triplet_minima sp_solve sp_lists sp_bmin8_reduce; do
+    python tools/summarise_sq.py "$O/sq_cf/run_counter_collection.csv" $K 16777216000 --what "c2match free $K" \
+      --out "$O/sq_cf_$K.json" | grep -E "valu_|wait_over|SQ_" | tr -d '\n'; echo
+  done ;;
 ab)
   for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
     for lib in $AB_LIBS; do
