@@ -1305,9 +1305,17 @@ def main():
         from oracle import oracle as O
         C, P = batch.n_cams, batch.n_pairs
         n_units, checked = 0, []
+        # allocations holding the same launch (C2: one launch per step, twenty
+        # allocations) are checked on different scenes of it: the m-th of n
+        # holders on scene m * scenes / n
+        holders = {}
+        for sl in sorted(slot_owner):
+            holders.setdefault(slot_owner[sl], []).append(sl)
         for sl in sorted(slot_owner):
             c = chunks[slot_owner[sl]]
-            s_first = c.s0
+            hs = holders[slot_owner[sl]]
+            s_in = hs.index(sl) * c.plan.n_scenes // len(hs)     # scene within the launch
+            s_first = c.s0 + s_in
             co = batch.cam_offs[s_first * C:(s_first + 1) * C + 1]
             pts1 = batch.pts[int(co[0]):int(co[-1])]
             out = out_slots[sl]
@@ -1315,11 +1323,14 @@ def main():
                 rd, ra, _, _, _ = O.pairwise(pts1, co - co[0], batch.F[s_first * P:(s_first + 1) * P],
                                              batch.pairs, 1, C)
                 # the scene's matrices, unpitched, read through the plan's offsets
-                gd = torch.cat([c.plan.matrix(out, 0, p).reshape(-1) for p in range(P)]).cpu().numpy()
+                gd = torch.cat([c.plan.matrix(out, s_in, p).reshape(-1) for p in range(P)]).cpu().numpy()
+                r0 = c.row_base + int(c.plan.row_offs_host[s_in * P])
             else:
                 rd, ra, _, _, _ = O.cube(pts1, co - co[0], batch.F[s_first * 3:(s_first + 1) * 3], 1)
-                gd = out[:rd.size].cpu().numpy()
-            ga = argmin[c.row_base:c.row_base + ra.size].cpu().numpy()
+                o0 = int(c.plan.cube_offs_host[s_in])
+                gd = out[o0:o0 + rd.size].cpu().numpy()
+                r0 = c.row_base + int(c.plan.row_offs_host[s_in])
+            ga = argmin[r0:r0 + ra.size].cpu().numpy()
             ok = np.array_equal(gd.view(np.int32), rd.view(np.int32)) and np.array_equal(ga, ra)
             parity_ok &= ok
             n_units += rd.size
@@ -1359,9 +1370,29 @@ def main():
                          "+ offsets + F, kernel, D2H argmin/min (best of 3); the distance matrices "
                          "stay in HBM")}
 
+    # ---- the kernel alone: a few launches of the first chunk, one at a time
+    # (HIP events around each, the stream drained between them), next to the
+    # timed period, which overlaps launch tails (steps / steps2 graphs) ------
+    kernel_iso = None
+    if env.is_root:
+        iso = []
+        for _ in range(5):
+            i0, i1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            i0.record(stream)
+            launch(chunks[0])
+            i1.record(stream)
+            torch.cuda.synchronize(dev)
+            iso.append(i0.elapsed_time(i1))
+        kernel_iso = {"ms": float(np.median(iso)), "min_ms": float(min(iso)),
+                      "launch_scenes": chunks[0].plan.n_scenes,
+                      "achieved": chunks[0].nbytes / (float(np.median(iso)) * 1e-3) / 1e9,
+                      "note": "median of 5 eager launches of the first launch's scenes, each alone "
+                              "on the launch stream between two HIP events"}
+
     # ---- achievable HBM write bandwidth on this box (same store form), over
     # the same output allocations the launches wrote ----------------------------
-    probe_gbs = None
+    probe_gbs = probe2_gbs = None
     if env.is_root:
         pe0, pe1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for buf in out_slots:
@@ -1379,6 +1410,21 @@ def main():
         pe1.record(stream)
         torch.cuda.synchronize(dev)
         probe_gbs = 5 * n_slots * max_units * 4 / (pe0.elapsed_time(pe1) * 1e-3) / 1e9
+        # steps2 times a two-stream period: the probe in the same shape too
+        # (even allocations on the launch stream, odd ones on a second)
+        if args.graph == "steps2":
+            alt = torch.cuda.Stream(dev)
+            q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            q0.record(stream)
+            alt.wait_stream(stream)
+            for rep in range(5):
+                for i, buf in enumerate(out_slots):
+                    with torch.cuda.stream(alt if i % 2 else stream):
+                        ops.hbm_write_probe(buf)
+            stream.wait_stream(alt)
+            q1.record(stream)
+            torch.cuda.synchronize(dev)
+            probe2_gbs = 5 * n_slots * max_units * 4 / (q0.elapsed_time(q1) * 1e-3) / 1e9
         if per_slot:
             for p in per_slot["slots"]:
                 t = float(np.mean([slot_ev[rep][p["slot"]][0].elapsed_time(slot_ev[rep][p["slot"]][1])
@@ -1474,7 +1520,12 @@ def main():
                             if step_graph is not None else "one event pair per launch"),
             "units_per_s_in_kernel": float(units_ev.sum() / durs.sum()),
             "write_probe_gbs": probe_gbs,
-            "frac_of_write_probe": (achieved_gbs / probe_gbs) if probe_gbs else None,
+            "frac_of_write_probe": ((achieved_gbs / probe2_gbs) if probe2_gbs else
+                                    (achieved_gbs / probe_gbs) if probe_gbs else None),
+            "write_probe_two_stream_gbs": probe2_gbs,
+            "probe_shape": ("two streams (even / odd allocations), as the steps2 graph runs its steps"
+                            if probe2_gbs else "one stream"),
+            "kernel_isolated": kernel_iso,
             # rank 0's launches of the kernel, in dispatch order: a rocprofv3
             # kernel trace of this command holds `before` launches, then the
             # `timed` ones this line's avg_launch_ms covers, then `after`
