@@ -1379,6 +1379,8 @@ def main():
         for _ in range(5):
             i0, i1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             torch.cuda.synchronize(dev)
+            if hasattr(torch.cuda, "_sleep"):
+                torch.cuda._sleep(2_000_000)   # the GPU waits ~1 ms: the launch is queued before i0 fires
             i0.record(stream)
             launch(chunks[0])
             i1.record(stream)
@@ -1388,7 +1390,8 @@ def main():
                       "launch_scenes": chunks[0].plan.n_scenes,
                       "achieved": chunks[0].nbytes / (float(np.median(iso)) * 1e-3) / 1e9,
                       "note": "median of 5 eager launches of the first launch's scenes, each alone "
-                              "on the launch stream between two HIP events"}
+                              "on the launch stream between two HIP events (the stream held by a "
+                              "~1 ms spin kernel while the host enqueues them)"}
 
     # ---- achievable HBM write bandwidth on this box (same store form), over
     # the same output allocations the launches wrote ----------------------------
