@@ -599,6 +599,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
             ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
             ch["cube"] = None
             ch["bm8"] = torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+            ch["bm32"] = torch.empty(max(tp.n_bm32, 4), dtype=torch.int32, device=dev)
         else:
             ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
             ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
@@ -622,7 +623,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                 ev[k][0].record(stream)
             if free:
                 ops.triplet_minima(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"], bmin8=ch["bm8"],
-                                   options=kernel_options)
+                                   bm32=ch["bm32"], options=kernel_options)
             else:
                 ops.triplet_cost_argmin(ch["pts"], ch["cam_offs"], ch["F"], ch["tplan"],
                                         out=(ch["cube"], ch["am"], ch["mv"]), options=kernel_options,
@@ -638,7 +639,8 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                 if ev:
                     ev[k][2].record(side)
                 if free:
-                    r, c, st = ops.linear_sum_assignment_resid(ch["lplan"], ch["tplan"], ch["bm8"],
+                    r, c, st = ops.linear_sum_assignment_resid(ch["lplan"], ch["tplan"],
+                                                               (ch["bm8"], ch["bm32"]),
                                                                options=kernel_options)
                 else:
                     bm8_args = ((ch["bm8"], ch["tplan"].bmin8_offs, ch["tplan"].segs)
@@ -757,11 +759,12 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
     cb = cube_bytes(counts)
     cost_bytes = 4.0 * triples
     if free:
-        # the minima pass: centroids + F in, 8-row minima + fp64 residuals out
-        ld = (counts.max() + 3) // 4 * 4
+        # the minima pass: centroids + F in; 8-row minima, block minima and
+        # fp64 residuals out
+        n_bm32 = sum(ch["tplan"].n_bm32 for ch in chunks)
         first_bytes = (16.0 * counts.sum() + 3 * 72.0 * len(N) + 2.0 * float(n_bmin8)
-                       + 8.0 * float((N * M + P * N + P * M).sum()))
-        lsap_bytes = 2.0 * float(n_bmin8)
+                       + 4.0 * float(n_bm32) + 8.0 * float((N * M + P * N + P * M).sum()))
+        lsap_bytes = 4.0 * float(n_bm32)
         first_kernel = "triplet_minima_kernel"
     else:
         first_bytes = cb
@@ -825,7 +828,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
         "lsap": {"problems": n_local, "shape": f"{int(counts[0, 0] * counts[0, 1])} x {int(counts[0, 2])}",
                  "ms_per_batch": lsap_ms, "ms_per_problem": lsap_ms / max(1, n_local),
                  "streamed_gb": lsap_bytes / 1e9, "cost_gb": cost_bytes / 1e9,
-                 "input": ("the 8-row minima + pair residuals (mvm_lsap_solve_resid)" if free
+                 "input": ("the minima pass's block minima + pair residuals (mvm_lsap_solve_resid)" if free
                            else "the cube kernel's 8-row minima (mvm_lsap_solve_ex3)"
                            if lsap_input == "bmin8" else "the cost cubes (mvm_lsap_solve_ex2)")},
         "matches_per_step": n_matches,

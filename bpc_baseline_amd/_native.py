@@ -116,7 +116,7 @@ SIGNATURES = {
         _vp, _sz, _vp, _vp]),               # workspace, bytes, options (host), stream
     "mvm_triplet_minima": (ctypes.c_int, [
         _vp, _vp, _vp, _i32, _i32,          # pts, cam_offs, F, n_scenes, max_n
-        _vp, _vp,                           # bmin8, bmin8_offs
+        _vp, _vp, _vp, _vp,                 # bmin8, bmin8_offs, bm32, bm32_offs
         _vp, _sz, _vp, _vp]),               # resid, resid_bytes, options (host), stream
     "mvm_lsap_plan": (_i64, [_i32, _vp, _vp, _vp, _vp]),
     "mvm_lsap_plan_ex": (_i64, [_i32, _vp, _vp, _i32, _vp, _vp]),
@@ -147,7 +147,7 @@ SIGNATURES = {
         _vp, _i32, _vp, _vp,                # dims, n, ws_offs, out_offs
         _vp, _sz, _vp, _vp, _vp,            # workspace, bytes, row_ind, col_ind, status
         _i64, _i64, _i64,                   # long_min, long_max, short_max
-        _vp, _vp, _vp,                      # bmin8, bmin8_offs, segs
+        _vp, _vp, _vp, _vp, _vp,            # bmin8, bmin8_offs, bm32, bm32_offs, segs
         _vp, _i32, _vp, _vp]),              # resid, max_n, options (host), stream
     "mvm_pack_detections": (ctypes.c_int, [
         _vp, _vp, _vp, _vp, _i32,           # boxes, conf, cls, img_offs, n_img

@@ -1482,34 +1482,43 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
 
 // --------------------------------------- cube-free 8-row minima (ABI 7) ----
 // For an assignment that never reads the cube itself (match_captures with
-// keep_cube=False, bench.py c2match): the 16-bit 8-row minima the fused
-// kernel writes next to the cube (CubeFusedArgs::bmin8), bit for bit, but
-// no cube -- plus every scene's fp64 pair residuals, from which the
-// assignment's kernels recompute the few entries they read (cube_f32):
-//   e12  [N][ld]  at resid + s * stride                  (i, j)
-//   e13T [P][ld]  at resid + s * stride + max_n * ld     (k, i)
-//   e23T [P][ld]  at resid + s * stride + 2 * max_n * ld (k, j)
-// stride = 3 * max_n * ld, ld = roundup(max_n, 4): mvm_triplet_workspace_bytes.
+// keep_cube=False, bench.py c2match), everything it needs instead of the cube:
+//   bmin8  the 16-bit 8-row minima the fused kernel writes next to the cube
+//          (CubeFusedArgs::bmin8), bit for bit;
+//   bm32   the 32-column block minima the candidate-list kernels start from,
+//          as upper bounds ((h << 16) | 0xFFFF of the block's smallest 16-bit
+//          key h, capped at +inf's key; sp_bmin8_reduce_kernel's values): per
+//          scene P rows of nb = ceil(M/32) * npad keys, npad = roundup(N, 16),
+//          block (jt, i) at jt * npad + i (rows i >= N: 0xFFFFFFFF, never a
+//          candidate), rows at bm32 + bm32_offs[s] + k * nb;
+//   resid  every scene's fp64 pair residuals, from which the assignment's
+//          kernels recompute the few entries they read (cube_f32):
+//            e12  [N][ld]  at resid + s * stride                  (i, j)
+//            e13T [P][ld]  at resid + s * stride + max_n * ld     (k, i)
+//            e23T [P][ld]  at resid + s * stride + 2 * max_n * ld (k, j)
+//          stride = 3 * max_n * ld, ld = roundup(max_n, 4).
 // RN(s / 3) and the float32 cast are monotone, so the minimum over a group's
 // 8 j of float32(third(s_j)) is float32(third(min_j s_j)): where every
-// residual of a chunk is <= 2^1020 (finite sums) a triple costs two fp64 adds
-// and one fp64 min, and the third runs once per (group, k) -- a quarter of the
-// fused kernel's VALU per triple and none of its 4 B/triple of stores.  Other
-// chunks compute every entry with cube_f32 and take the minimum of the keys
-// (NaN -> key 0), as the fused kernel does.
-// A workgroup owns (scene, 32 consecutive j: one 8-row group per wave) and
-// walks the scene's i rows in chunks of IB, so the wave's e23 registers (8 j x
-// 4 k per lane, the prologue's largest part) are computed once per 256 i rows
-// instead of once per 16; per chunk the e13 [IB][P] and e12 [IB][32] tiles go
-// through LDS (every residual with row_safe's arithmetic, like the fused
-// kernel's prologue).  The workgroups of j block 0 write e13T; every one writes
-// its e23T rows and e12 columns.
+// residual is <= 2^1020 (finite sums) a triple costs two fp64 adds and one
+// fp64 min, and the third runs once per (group, k) -- a quarter of the fused
+// kernel's VALU per triple and none of its 4 B/triple of stores.  Elsewhere
+// every entry is computed exactly (third_q, the division for non-finite sums)
+// and the minimum taken over the keys (NaN -> key 0), as the fused kernel does.
+// A workgroup owns (scene, one 32-column block jb of j); thread t takes the
+// short-side column k = t (P <= 256) for all 32 j of the block, so a block's
+// minimum (four 8-row groups) is one thread's, and e13[i][k] is the thread's
+// own value: per chunk of IB rows i only the chunk's row lines and its e12
+// [IB][32] tile go through LDS.  The e23 column (32 j) sits in the thread's
+// registers for the whole scene.  Workgroups of block 0 write e13T, every
+// workgroup its e23T rows and e12 columns.
 struct MinimaArgs {
     const double *pts;
     const int64_t *cam_offs;
     const double *F;            // [S*3, 9]: F12, F13, F23
     uint16_t *bmin8;
     const int64_t *bmin8_offs;
+    uint32_t *bm32;
+    const int64_t *bm32_offs;
     double *resid;
     int64_t stride;             // doubles per scene
     int32_t ld;                 // row stride of e12 / e13T / e23T (multiple of 4)
@@ -1518,23 +1527,15 @@ struct MinimaArgs {
 };
 
 template <int IB>
-__global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_kernel(MinimaArgs args) {
-    constexpr int RPW = 8;                     // j rows per wave: one 8-row group
-    constexpr int kJ = kWaves * RPW;           // j per workgroup
-    struct ColRec {
-        LineRec l;
-        double x, y;
-    };
-    __shared__ __attribute__((aligned(16))) double s13[IB][kChunk];   // 32 KiB at IB 16
+__global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs args) {
+    constexpr int kJ = 32;                     // j per workgroup: four 8-row groups
+    static_assert(IB == 16, "the chunk's block minima leave as one 64-byte run per k");
     __shared__ __attribute__((aligned(16))) double s12[IB][kJ];
     __shared__ LineRec s_r13[IB], s_r12[IB], s_c12[kJ], s_r23[kJ];
     __shared__ double s_p0[IB][2], s_p1[kJ][2];
-    static_assert(sizeof(ColRec) * kChunk <= sizeof(s13), "F23 column scratch fits s13");
-    ColRec *s_c23 = reinterpret_cast<ColRec *>(&s13[0][0]);
+    __shared__ __attribute__((aligned(16))) uint32_t s_bm[IB][kThreads];   // the chunk's block minima
 
     const int t = threadIdx.x;
-    const int wave = __builtin_amdgcn_readfirstlane(t / kWave);
-    const int lane = t % kWave;
     uint32_t blk = blockIdx.x;   // each XCD a contiguous range of (scene, j block)s
     {
         const uint32_t nb = gridDim.x, q = nb / 8, r = nb % 8, x = blk % 8;
@@ -1547,9 +1548,9 @@ __global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_ker
     const int N = (int)(c1 - c0), M = (int)(c2 - c1), P = (int)(co[3] - c2);
     const int jw0 = jb * kJ;
     if (jw0 >= M || N == 0 || P == 0) return;   // uniform; an empty problem reads no cost
-    const int j0 = jw0 + wave * RPW;
-    const int nrows = min(RPW, M - j0);          // uniform per wave, may be <= 0
-    const int kb = kColsPerLane * lane, kvalid = P - kb;
+    const int nj = min(kJ, M - jw0);             // j rows of this block (uniform)
+    const int k = t;
+    const bool kv = k < P;
     const double *F12 = args.F + (3 * (int64_t)s + 0) * 9;
     const double *F13 = args.F + (3 * (int64_t)s + 1) * 9;
     const double *F23 = args.F + (3 * (int64_t)s + 2) * 9;
@@ -1558,48 +1559,42 @@ __global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_ker
     double *E13T = E12 + (int64_t)args.max_n * ld;
     double *E23T = E13T + (int64_t)args.max_n * ld;
     const int g8 = (M + 7) / 8;
-    const int64_t boff = args.bmin8_offs[s];
-    uint16_t *B8 = args.bmin8 + boff;
-    const bool vec = ((P & 3) == 0) && ((boff & 3) == 0);   // 8-byte key stores
+    uint16_t *B8 = args.bmin8 + args.bmin8_offs[s];
+    const int npad = (N + 15) & ~15;
+    const int nbk = ((M + 31) / 32) * npad;
+    uint32_t *BM = args.bm32 + args.bm32_offs[s] + (int64_t)k * nbk + (int64_t)jb * npad;
 
-    // ---- once per workgroup: the j block's lines and every k column's ----
+    // ---- once per workgroup: the block's j lines, this thread's k lines -----
     bool any_deg = false;
-    if (t >= kWave && t < kWave + kJ) {
-        const int jj = t - kWave;
+    if (t < kJ) {
         LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
         double px = 0.0, py = 0.0;
-        if (jw0 + jj < M) {
+        if (t < nj) {
             double f[9];
-            px = args.pts[2 * (c1 + jw0 + jj)];
-            py = args.pts[2 * (c1 + jw0 + jj) + 1];
+            px = args.pts[2 * (c1 + jw0 + t)];
+            py = args.pts[2 * (c1 + jw0 + t) + 1];
             load_f(F12, f);
             a.deg = col_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
             load_f(F23, f);
             b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
         }
         any_deg |= (a.deg != 0.0) || (b.deg != 0.0);
-        s_c12[jj] = a;
-        s_r23[jj] = b;
-        s_p1[jj][0] = px;
-        s_p1[jj][1] = py;
+        s_c12[t] = a;
+        s_r23[t] = b;
+        s_p1[t][0] = px;
+        s_p1[t][1] = py;
     }
-    LineRec cl13{0.0, 0.0, 0.0, 0.0};   // column k = t, F13 (registers, for e13)
+    LineRec cl13{0.0, 0.0, 0.0, 0.0}, c23{0.0, 0.0, 0.0, 0.0};
     double kx = 0.0, ky = 0.0;
-    {
-        ColRec c23{{0.0, 0.0, 0.0, 0.0}, 0.0, 0.0};
-        if (t < P) {
-            double f[9];
-            kx = args.pts[2 * (c2 + t)];
-            ky = args.pts[2 * (c2 + t) + 1];
-            load_f(F13, f);
-            cl13.deg = col_line(f, kx, ky, cl13.l0, cl13.l1, cl13.l2) ? 1.0 : 0.0;
-            load_f(F23, f);
-            c23.l.deg = col_line(f, kx, ky, c23.l.l0, c23.l.l1, c23.l.l2) ? 1.0 : 0.0;
-            c23.x = kx;
-            c23.y = ky;
-            any_deg |= (cl13.deg != 0.0) || (c23.l.deg != 0.0);
-        }
-        s_c23[t] = c23;
+    if (kv) {
+        double f[9];
+        kx = args.pts[2 * (c2 + k)];
+        ky = args.pts[2 * (c2 + k) + 1];
+        load_f(F13, f);
+        cl13.deg = col_line(f, kx, ky, cl13.l0, cl13.l1, cl13.l2) ? 1.0 : 0.0;
+        load_f(F23, f);
+        c23.deg = col_line(f, kx, ky, c23.l0, c23.l1, c23.l2) ? 1.0 : 0.0;
+        any_deg |= (cl13.deg != 0.0) || (c23.deg != 0.0);
     }
     // uniform: no j / k line of the workgroup is degenerate (the rows' lines
     // are judged per chunk)
@@ -1611,44 +1606,31 @@ __global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_ker
                           line_dist(row.l0, row.l1, row.l2, cx, cy));   // :28
         return pair_e(col, row, rx, ry, cx, cy);
     };
-    // rows past the view (the last group of a view whose M is not a multiple
-    // of 8) hold e23 = +inf: their sums are +inf (or NaN where a valid row of
-    // the same k is NaN too), so they never decide a group's minimum and the
-    // loops below need no per-row test
-    bool tame23 = true;   // every e23 of this thread's rows is <= kTameResidual
-    double a23[RPW][kColsPerLane];
+    // e23[j][k] of the block's 32 j; rows past the view hold +inf, so they
+    // never decide a group's minimum (their sums are +inf, or NaN where a
+    // valid row of the same k is NaN too)
+    bool tame = true;
+    double a23[kJ];
 #pragma unroll
-    for (int q = 0; q < kColsPerLane; ++q) {
-        const ColRec cl = s_c23[min(kb + q, kChunk - 1)];
+    for (int jj = 0; jj < kJ; ++jj) {
+        a23[jj] = jj >= nj ? (double)INFINITY
+                  : kv      ? pair(!deg_fixed, c23, s_r23[jj], s_p1[jj][0], s_p1[jj][1], kx, ky)
+                            : 0.0;
+        tame &= jj >= nj || a23[jj] <= kTameResidual;
+    }
+    if (kv) {                                    // e23T row k: the block's j (256 contiguous bytes)
+        double *dst = E23T + (int64_t)k * ld + jw0;
+        if (nj == kJ) {
 #pragma unroll
-        for (int r = 0; r < RPW; ++r) {
-            const int jj = wave * RPW + r;
-            a23[r][q] = r >= nrows  ? (double)INFINITY
-                        : kb + q < P ? pair(!deg_fixed, cl.l, s_r23[jj], s_p1[jj][0], s_p1[jj][1], cl.x, cl.y)
-                                     : 0.0;
-            tame23 &= r >= nrows || a23[r][q] <= kTameResidual;
+            for (int jj = 0; jj < kJ; jj += 2) *reinterpret_cast<f64x2 *>(dst + jj) = f64x2{a23[jj], a23[jj + 1]};
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < kJ; ++jj)
+                if (jj < nj) dst[jj] = a23[jj];
         }
     }
-    // e23T rows k = kb + q, columns j0 .. j0 + 7 (64 contiguous bytes)
-    if (nrows > 0) {
-#pragma unroll
-        for (int q = 0; q < kColsPerLane; ++q) {
-            if (kb + q >= P) continue;
-            double *dst = E23T + (int64_t)(kb + q) * ld + j0;
-            if (nrows == RPW) {
-#pragma unroll
-                for (int r = 0; r < RPW; r += 2)
-                    *reinterpret_cast<f64x2 *>(dst + r) = f64x2{a23[r][q], a23[r + 1][q]};
-            } else {
-#pragma unroll
-                for (int r = 0; r < RPW; ++r)
-                    if (r < nrows) dst[r] = a23[r][q];
-            }
-        }
-    }
-    __syncthreads();   // every wave has read its F23 columns: s13 is free for e13
 
-    // ---- the scene's i rows, IB at a time ------------------------------------
+    // ---- the scene's i rows, IB at a time --------------------------------------
     for (int i0 = 0; i0 < N; i0 += IB) {
         const int ni = min(IB, N - i0);
         bool deg_rows = false;
@@ -1672,91 +1654,79 @@ __global__ __launch_bounds__(kThreads, IB <= 16 ? 4 : 2) void triplet_minima_ker
             s_p0[t][1] = py;
         }
         // (the barrier also puts every wave past the previous chunk's reads of
-        // s13 / s12: it must run whatever deg_fixed is -- no short circuit)
+        // s12: it must run whatever deg_fixed is -- no short circuit)
         const bool deg_chunk = __syncthreads_or(deg_rows) != 0;
         const bool nd = !deg_fixed && !deg_chunk;
-        bool tame = tame23;
-        if (t < P) {
-#pragma unroll 2
-            for (int r = 0; r < IB; r += 2) {
-                const double ea =
-                    r < ni ? pair(nd, cl13, s_r13[r], s_p0[r][0], s_p0[r][1], kx, ky) : 0.0;
-                const double eb =
-                    r + 1 < ni ? pair(nd, cl13, s_r13[r + 1], s_p0[r + 1][0], s_p0[r + 1][1], kx, ky) : 0.0;
-                s13[r][t] = ea;
-                s13[r + 1][t] = eb;
-                tame &= (ea <= kTameResidual) && (eb <= kTameResidual);
-                if (jb == 0) {                     // e13T row k = t: i0 + r, i0 + r + 1
-                    double *dst = E13T + (int64_t)t * ld + i0 + r;
-                    if (r + 1 < ni) *reinterpret_cast<f64x2 *>(dst) = f64x2{ea, eb};
-                    else if (r < ni) dst[0] = ea;
-                }
-            }
-        } else {
-            for (int r = 0; r < IB; ++r) s13[r][t] = 0.0;   // lanes past P read zeros
-        }
+        bool tame_c = tame;
         for (int x = t; x < IB * kJ; x += kThreads) {
             const int r = x / kJ, jj = x % kJ;
-            const bool v = r < ni && jw0 + jj < M;
+            const bool v = r < ni && jj < nj;
             const double e =
                 v ? pair(nd, s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1]) : 0.0;
             s12[r][jj] = e;
-            tame &= e <= kTameResidual;
+            tame_c &= e <= kTameResidual;
             if (v) E12[(int64_t)(i0 + r) * ld + jw0 + jj] = e;
         }
-        // every sum of the chunk is finite when its residuals are <= 2^1020
-        // (NaN fails the compare): the minimum of the sums, then one third
-        const bool fast = __syncthreads_and(tame) != 0;
-        if (nrows <= 0) continue;                  // uniform per wave (barriers above only)
+        const bool chunk_fast = __syncthreads_and(tame_c) != 0;
         for (int ii = 0; ii < ni; ++ii) {
-            double a13[kColsPerLane];
-            {
-                const f64x2 lo = *reinterpret_cast<const f64x2 *>(&s13[ii][kb]);
-                const f64x2 hi = *reinterpret_cast<const f64x2 *>(&s13[ii][kb + 2]);
-                a13[0] = lo.x;
-                a13[1] = lo.y;
-                a13[2] = hi.x;
-                a13[3] = hi.y;
-            }
-            double v12[RPW];
-#pragma unroll
-            for (int r = 0; r < RPW; r += 2) {
-                const f64x2 w = *reinterpret_cast<const f64x2 *>(&s12[ii][wave * RPW + r]);
-                v12[r] = w.x;
-                v12[r + 1] = w.y;
-            }
-            uint32_t key[kColsPerLane];
+            const int i = i0 + ii;
+            const double e13 = kv ? pair(nd, cl13, s_r13[ii], s_p0[ii][0], s_p0[ii][1], kx, ky) : 0.0;
+            if (jb == 0 && kv) E13T[(int64_t)k * ld + i] = e13;
+            // every sum of the wave's rows is finite (wave-uniform)
+            const bool fast = chunk_fast && __all(e13 <= kTameResidual);
+            // the four groups' keys (a group past the view -- all its e23
+            // +inf -- is computed and ignored below)
+            uint32_t key[kJ / 8];
             if (fast) {
 #pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
-                    double m = (v12[0] + a13[q]) + a23[0][q];          // (e12 + e13) + e23, :81
+                for (int g = 0; g < kJ / 8; ++g) {
+                    double sm[8];
 #pragma unroll
-                    for (int r = 1; r < RPW; ++r) m = fmin(m, (v12[r] + a13[q]) + a23[r][q]);
-                    key[q] = __float_as_uint((float)third_q(m)) | 0x80000000u;
+                    for (int r = 0; r < 8; r += 2) {
+                        const f64x2 w = *reinterpret_cast<const f64x2 *>(&s12[ii][8 * g + r]);
+                        sm[r] = (w.x + e13) + a23[8 * g + r];              // (e12 + e13) + e23, :81
+                        sm[r + 1] = (w.y + e13) + a23[8 * g + r + 1];
+                    }
+                    // a tree: the same minimum (no NaN here), three dependent steps
+                    const double m = fmin(fmin(fmin(sm[0], sm[1]), fmin(sm[2], sm[3])),
+                                          fmin(fmin(sm[4], sm[5]), fmin(sm[6], sm[7])));
+                    key[g] = __float_as_uint((float)third_q(m)) | 0x80000000u;
                 }
-            } else {   // a chunk with a huge / non-finite residual: every entry exactly
-#pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q) {
+            } else {   // a huge / non-finite residual: every entry exactly
+#pragma unroll 1
+                for (int g = 0; g < kJ / 8; ++g) {
                     uint32_t kk = 0xFFFFFFFFu;
 #pragma unroll
-                    for (int r = 0; r < RPW; ++r) {
-                        const double sum = (v12[r] + a13[q]) + a23[r][q];
+                    for (int r = 0; r < 8; ++r) {
+                        const double sum = (s12[ii][8 * g + r] + e13) + a23[8 * g + r];
                         double qv = third_q(sum);
                         qv = third_ok(qv) ? qv : sum / 3.0;
                         kk = umin(kk, bm8_key((float)qv));
                     }
-                    key[q] = kk;
+                    key[g] = kk;
                 }
             }
-            uint16_t *brow = B8 + ((int64_t)(i0 + ii) * g8 + j0 / 8) * P;
-            if (vec && kvalid >= kColsPerLane) {
-                *reinterpret_cast<uint2 *>(brow + kb) =
-                    make_uint2((key[0] >> 16) | (key[1] & 0xFFFF0000u), (key[2] >> 16) | (key[3] & 0xFFFF0000u));
-            } else {
+            uint32_t hmin = 0xFFFFu;             // the block's smallest 16-bit key
 #pragma unroll
-                for (int q = 0; q < kColsPerLane; ++q)
-                    if (q < kvalid) brow[kb + q] = (uint16_t)(key[q] >> 16);
+            for (int g = 0; g < kJ / 8; ++g) {
+                if (8 * g < nj) {                // uniform
+                    const uint32_t h = key[g] >> 16;
+                    hmin = umin(hmin, h);
+                    if (kv) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
+                }
             }
+            // sp_bmin8_reduce_kernel's upper bound of the block minimum
+            s_bm[ii][t] = umin((hmin << 16) | 0xFFFFu, 0xFF800000u);
+        }
+        // the chunk's 16 block minima of column k: one 64-byte run (rows past
+        // the view never a candidate)
+        if (kv) {
+            uint32_t v[IB];
+#pragma unroll
+            for (int ii = 0; ii < IB; ++ii) v[ii] = ii < ni ? s_bm[ii][t] : 0xFFFFFFFFu;
+#pragma unroll
+            for (int ii = 0; ii < IB; ii += 4)
+                *reinterpret_cast<uint4 *>(BM + i0 + ii) = make_uint4(v[ii], v[ii + 1], v[ii + 2], v[ii + 3]);
         }
     }
 }
@@ -1842,8 +1812,9 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
 
 int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                        int32_t n_scenes, int32_t max_n, uint16_t *bmin8_dev,
-                       const int64_t *bmin8_offs_dev, double *resid_dev, size_t resid_bytes,
-                       const mvm_options *opts, mvm_stream_t stream) {
+                       const int64_t *bmin8_offs_dev, uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
+                       double *resid_dev, size_t resid_bytes, const mvm_options *opts,
+                       mvm_stream_t stream) {
     mvm_clear_error();
     mvm_options o;
     int st = mvm_resolve_options(opts, o);
@@ -1853,8 +1824,11 @@ int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const
         return mvm_fail(MVM_ERR_UNSUPPORTED, "mvm_triplet_minima: views of at most %d detections "
                         "(%d given)", kChunk, (int)max_n);
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
-    if (!pts_dev || !cam_offs_dev || !F_dev || !bmin8_dev || !bmin8_offs_dev || !resid_dev)
+    if (!pts_dev || !cam_offs_dev || !F_dev || !bmin8_dev || !bmin8_offs_dev || !bm32_dev ||
+        !bm32_offs_dev || !resid_dev)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
+    if (((uintptr_t)bm32_dev & 15) != 0)
+        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "bm32 not 16-byte aligned");
     const size_t need = mvm_triplet_workspace_bytes(n_scenes, max_n);
     if (resid_bytes < need)
         return mvm_fail(MVM_ERR_WORKSPACE, "residual workspace %zu bytes < required %zu", resid_bytes, need);
@@ -1866,22 +1840,17 @@ int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const
     a.F = F_dev;
     a.bmin8 = bmin8_dev;
     a.bmin8_offs = bmin8_offs_dev;
+    a.bm32 = bm32_dev;
+    a.bm32_offs = bm32_offs_dev;
     a.resid = resid_dev;
     a.ld = (max_n + 3) / 4 * 4;
     a.max_n = max_n;
     a.stride = (int64_t)3 * max_n * a.ld;
-    a.j_blocks = (max_n + kWaves * 8 - 1) / (kWaves * 8);
-    if (o.cube_tile_rows != 0 && o.cube_tile_rows != 16 && o.cube_tile_rows != 32)
-        return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "cube_tile_rows %d not 0, 16 or 32", (int)o.cube_tile_rows);
+    a.j_blocks = (max_n + 31) / 32;
     const int64_t blocks = (int64_t)n_scenes * a.j_blocks;
     if ((st = grid_check(blocks))) return st;
-    const hipStream_t hs = reinterpret_cast<hipStream_t>(stream);
-    // i rows per chunk (mvm_options.cube_tile_rows): 16 by default (four
-    // workgroups per CU), 32 halves the per-chunk barriers and row lines (two)
-    if (o.cube_tile_rows == 32)
-        triplet_minima_kernel<32><<<dim3((unsigned)blocks), dim3(kThreads), 0, hs>>>(a);
-    else
-        triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0, hs>>>(a);
+    triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0,
+                                reinterpret_cast<hipStream_t>(stream)>>>(a);
     return mvm_check_launch("triplet_minima_kernel");
 }
 

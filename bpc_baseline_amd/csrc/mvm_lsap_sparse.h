@@ -48,6 +48,12 @@ struct LsapSparseArgs {
     int64_t resid_stride = 0;     // doubles per scene (3 * max_n * ld)
     int32_t resid_ld = 0;
     int32_t resid_rows = 0;       // max_n: e13T starts max_n * ld after e12
+    // ... and its block minima as mvm_triplet_minima wrote them (no reduction
+    // pass, no block minima in the workspace): row s of problem p at bm32 +
+    // bm32_offs[p] + s * ceil(seg/32) * roundup(L/seg, 16), block (jt, g) at
+    // jt * roundup(L/seg, 16) + g
+    const uint32_t *bm32 = nullptr;
+    const int64_t *bm32_offs = nullptr;
 };
 
 // status of a problem that cannot be solved as given (ABI 7): its short side
@@ -81,8 +87,10 @@ struct SpLayout {
 // free ties at the sink, rows whose list overflowed kSpLCap, Dijkstra steps
 constexpr int kSpStats = 4;
 
-// tr: the problem is tall (transposed, short side = columns)
-__host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, size_t elem, bool tr) {
+// tr: the problem is tall (transposed, short side = columns); ext_bm: its
+// block minima come from outside the workspace (LsapSparseArgs::bm32)
+__host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, size_t elem, bool tr,
+                                                       bool ext_bm = false) {
     SpLayout y;
     size_t o = 0;
     auto take = [&](size_t bytes) {
@@ -99,7 +107,7 @@ __host__ __device__ inline SpLayout lsap_sparse_layout(int64_t S, int64_t L, siz
     const int64_t nt = (L + kSpTileCols - 1) / kSpTileCols;
     y.stats = take(kSpStats * 4);
     y.flags = take((size_t)(nt > 32 ? nt : 32) * 4);   // invalid-entry flag per tile
-    y.bm = take((size_t)S * nb * elem);              // ordered keys of the block minima
+    y.bm = take(ext_bm ? 0 : (size_t)S * nb * elem);   // ordered keys of the block minima
     y.lcol = take((size_t)S * kSpLCap * 4);
     y.lval = take((size_t)S * kSpLCap * elem);
     y.ln = take((size_t)S * 4);                      // list length (-1: dense row)

@@ -212,7 +212,7 @@ __global__ __launch_bounds__(kSpNT) void sp_blockmin_kernel(LsapSparseArgs a, in
     const int j0 = w * kSpTileCols;
     if (j0 >= L) return;
     const int j1 = min(j0 + kSpTileCols, L);
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr, a.bm32 != nullptr);
     unsigned char *ws = a.ws + a.ws_offs[p];
     KT *bm = reinterpret_cast<KT *>(ws + y.bm);
     const CT *C0 = reinterpret_cast<const CT *>(a.cost) + a.cost_offs[p];
@@ -459,9 +459,9 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     if (!lsap_sparse_class(a.lo, a.wave_max, R, Kd)) return;
     const bool tr = Kd < R;
     const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr, a.bm32 != nullptr);
     unsigned char *ws = a.ws + a.ws_offs[p];
-    const KT *bm = reinterpret_cast<const KT *>(ws + y.bm);
+    const bool ext = a.bm32 != nullptr && sizeof(CT) == 4;   // block minima from mvm_triplet_minima
     int32_t *lcol = reinterpret_cast<int32_t *>(ws + y.lcol);
     CT *lval = reinterpret_cast<CT *>(ws + y.lval);
     int32_t *ln = reinterpret_cast<int32_t *>(ws + y.ln);
@@ -471,9 +471,24 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     const int seg0 = lsap_sparse_seg(a, p, tr, L), seg = seg0 ? seg0 : L;
     bool src_ok;
     const SpSrc<CT> src = sp_src<CT>(a, p, tr, S, L, seg0, src_ok);
-    if (!src_ok) return;                                   // sp_solve_kernel reports it
-    const int bps = (seg + kSpBlock - 1) / kSpBlock, nb = (L / seg) * bps;
-    const float rbps = 1.0f / (float)bps;
+    if (!src_ok || (ext && !seg0)) return;                 // sp_solve_kernel reports it
+    const int bps = (seg + kSpBlock - 1) / kSpBlock, nseg = L / seg;
+    // ext: block b = jt * npad + g (rows g >= nseg padding, 0xFFFFFFFF);
+    // else b = g * bps + jt
+    const int npad = ext ? (nseg + 15) & ~15 : nseg;
+    const int nb = npad * bps;
+    const float rbps = 1.0f / (float)bps, rnpad = 1.0f / (float)npad;
+    auto decode = [&](int b, int &jt) {                    // -> segment g, part jt
+        if (ext) {
+            int g;
+            jt = sp_div(b, npad, rnpad, g);
+            return g;
+        }
+        return sp_div(b, bps, rbps, jt);
+    };
+    const KT *bm = ext ? reinterpret_cast<const KT *>(a.bm32 + a.bm32_offs[p])
+                       : reinterpret_cast<const KT *>(ws + y.bm);
+    int bad = 0;                                           // ext: a NaN entry (key 0) in these rows
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int s = grp * (kSpNT / 64) + wave; s < S; s += kSpRowGroups * (kSpNT / 64)) {
         KT k[kQ];
@@ -481,6 +496,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         for (int q = 0; q < kQ; ++q) {
             const int idx = lane + 64 * q;
             k[q] = idx < nb ? bm[(int64_t)s * nb + idx] : K::kMax;
+            if (ext) bad |= !(k[q] >> (8 * sizeof(KT) - 1));   // a NaN's key: below every value's
         }
         KT thr = K::kMax;
         CT theta = (CT)INFINITY;
@@ -518,7 +534,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                         s_cand[wave][pos] = lane + 64 * q;
                     } else {                                // its first column | its width << 16
                         int jt;
-                        const int g = sp_div(lane + 64 * q, bps, rbps, jt);
+                        const int g = decode(lane + 64 * q, jt);
                         s_cand[wave][pos] = (g * seg + jt * kSpBlock) | (min(kSpBlock, seg - jt * kSpBlock) << 16);
                     }
                 }
@@ -541,9 +557,9 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                 int e = 0;
                 if (idx < ncand) {
                     int jt;
-                    const int g = sp_div(s_cand[wave][idx], bps, rbps, jt);
+                    const int g = decode(s_cand[wave][idx], jt);
                     const int g8 = 4 * jt + u;
-                    if (g8 < bps8) {
+                    if (g8 < bps8 && g < nseg) {            // (padding rows: never candidates)
                         c = ((KT)B8[(int64_t)(g * bps8 + g8) * S + s] << 16) <= thr;
                         e = (g * seg + 8 * g8) | (min(8, seg - 8 * g8) << 16);
                     }
@@ -595,6 +611,10 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             ln[s] = cnt <= kSpLCap ? cnt : -1;
             theta_out[s] = theta;
         }
+    }
+    if (ext) {                                             // this row group's NaN flag
+        bad = __syncthreads_or(bad);
+        if (threadIdx.x == 0) reinterpret_cast<int32_t *>(ws + y.flags)[grp] = bad;
     }
 }
 
@@ -666,7 +686,7 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
         if (threadIdx.x == 0) a.status[p] = kSpStatusBounds;
         return;
     }
-    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr);
+    const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr, a.bm32 != nullptr);
     const unsigned char *ws = a.ws + a.ws_offs[p];
     const int32_t *lcol = reinterpret_cast<const int32_t *>(ws + y.lcol);
     const CT *lval = reinterpret_cast<const CT *>(ws + y.lval);
@@ -693,8 +713,9 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
     // NaN / -inf anywhere (sp_blockmin_kernel's tile flags): scipy's ValueError
     {
         const int seg = lsap_sparse_seg(a, p, tr, L);      // whose tiles wrote the flags
-        const int nt = seg ? ((L / seg) * ((seg + kSpBlock - 1) / kSpBlock) + 63) / 64
-                           : (L + kSpTileCols - 1) / kSpTileCols;
+        const int nt = a.bm32 ? kSpRowGroups                // sp_lists_kernel's row groups
+                       : seg  ? ((L / seg) * ((seg + kSpBlock - 1) / kSpBlock) + 63) / 64
+                              : (L + kSpTileCols - 1) / kSpTileCols;
         const int32_t *fl = reinterpret_cast<const int32_t *>(ws + y.flags);
         int bad = 0;
         for (int x = t; x < nt; x += kSpNT) bad |= fl[x];
@@ -1052,11 +1073,13 @@ int sp_launch(const LsapSparseArgs &a0, int32_t n, int64_t long_max, hipStream_t
         a.bmin8_offs = nullptr;
         a.segs = nullptr;
         a.resid = nullptr;
+        a.bm32 = nullptr;
+        a.bm32_offs = nullptr;
     }
     // cube-free: every problem of the class takes its block minima from the
     // 8-row minima (a problem that cannot is refused by sp_solve_kernel)
     if (!a.resid) sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
-    if (a.bmin8)
+    if (a.bmin8 && !a.bm32)
         sp_bmin8_reduce_kernel<<<dim3((unsigned)(n * (kSpMaxBlocks / 64))), dim3(kSpNT), 0, s>>>(a, n);
     sp_lists_kernel<CT><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
     const int cap = a.s_cap;
@@ -1116,7 +1139,7 @@ int64_t mvm_lsap_plan_resid(int32_t n_problems, const int64_t *rows, const int64
         const int64_t nr = tr ? cols[p] : rows[p], nc = tr ? rows[p] : cols[p];
         // only the candidate-list class's lists (no transposed cost: there is none)
         if (rows[p] && cols[p] && nc <= kSpMaxCols && nr <= kSpMaxShort)
-            w += (int64_t)lsap_sparse_layout(nr, nc, sizeof(float), tr).total;
+            w += (int64_t)lsap_sparse_layout(nr, nc, sizeof(float), tr, true).total;
         o += rows[p] < cols[p] ? rows[p] : cols[p];
     }
     ws_offs[n_problems] = w;
@@ -1129,6 +1152,7 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
                          int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                          int64_t long_min, int64_t long_max, int64_t short_max,
                          const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
+                         const uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
                          const int64_t *segs_dev, const double *resid_dev, int32_t max_n,
                          const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();
@@ -1159,8 +1183,8 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
                             "all of the candidate-list class (long sides >= %d, > %d, <= %d; short sides "
                             "<= %d)", (long long)long_min, (long long)long_max, (long long)short_max, sp_lo,
                             wave_max, kSpMaxCols, kSpMaxShort);
-        if (!bmin8_dev || !bmin8_offs_dev || !segs_dev || !resid_dev || !workspace_dev || !row_ind_dev ||
-            !col_ind_dev)
+        if (!bmin8_dev || !bmin8_offs_dev || !bm32_dev || !bm32_offs_dev || !segs_dev || !resid_dev ||
+            !workspace_dev || !row_ind_dev || !col_ind_dev)
             return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     }
     (void)workspace_bytes;   // the per-problem regions come from mvm_lsap_plan_resid's offsets
@@ -1174,6 +1198,8 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
     sa.resid_ld = ld;
     sa.resid_rows = max_n;
     sa.resid_stride = (int64_t)3 * max_n * ld;
+    sa.bm32 = bm32_dev;
+    sa.bm32_offs = bm32_offs_dev;
     return sp_launch<float>(sa, n_problems, long_max < 1 ? 1 : long_max,
                             reinterpret_cast<hipStream_t>(stream));
 }

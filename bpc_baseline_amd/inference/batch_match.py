@@ -166,11 +166,11 @@ def _device_chain(pts, cam_offs, cam_offs_host, F_dev, proj_dev, S, threshold, c
     if cube_free:
         # the assignment never reads a cube: the 8-row minima it reduces and
         # the fp64 pair residuals it recomputes its entries from
-        bm8 = ops.triplet_minima(pts, cam_offs, F_dev, plan)
+        minima = ops.triplet_minima(pts, cam_offs, F_dev, plan)
         mark("cube")
         lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
         mark("lsap plan")
-        row_ind, col_ind, lstat = ops.linear_sum_assignment_resid(lplan, plan, bm8)
+        row_ind, col_ind, lstat = ops.linear_sum_assignment_resid(lplan, plan, minima)
         mark("lsap")
         match, cost, X, count = ops.select_triangulate_resid(plan, cam_offs, lplan.out_offs, row_ind,
                                                              col_ind, pts, proj_dev, threshold)

@@ -276,22 +276,23 @@ def _(cost, cost_offs, dims, ws_offs, out_offs, workspace, row_ind, col_ind, sta
 
 @torch.library.custom_op("mvmatch::triplet_minima_out", mutates_args=("bmin8", "resid"))
 def triplet_minima_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, max_n: int,
-                       bmin8: Tensor, bmin8_offs: Tensor, resid: Tensor,
-                       opts: Optional[List[int]] = None) -> None:
-    """The cube's 8-row minima + every scene's fp64 pair residuals, no cube
-    (mvm_triplet_minima, ABI 7)."""
+                       bmin8: Tensor, bmin8_offs: Tensor, bm32: Tensor, bm32_offs: Tensor,
+                       resid: Tensor, opts: Optional[List[int]] = None) -> None:
+    """The cube's 8-row minima, the assignment's 32-column block minima and
+    every scene's fp64 pair residuals, no cube (mvm_triplet_minima, ABI 7)."""
     _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
     for t, n, dt in ((bmin8, "bmin8", torch.int16), (bmin8_offs, "bmin8_offs", torch.int64),
+                     (bm32, "bm32", torch.int32), (bm32_offs, "bm32_offs", torch.int64),
                      (resid, "resid", torch.uint8)):
         _require(t, n, dt, pts.device)
     st = _native.load().mvm_triplet_minima(_p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(bmin8),
-                                           _p(bmin8_offs), _p(resid), resid.numel(), _opts_ref(opts),
-                                           _stream(pts))
+                                           _p(bmin8_offs), _p(bm32), _p(bm32_offs), _p(resid),
+                                           resid.numel(), _opts_ref(opts), _stream(pts))
     _native.check("mvm_triplet_minima", st)
 
 
 @triplet_minima_out.register_fake
-def _(pts, cam_offs, F, n_scenes, max_n, bmin8, bmin8_offs, resid, opts=None):
+def _(pts, cam_offs, F, n_scenes, max_n, bmin8, bmin8_offs, bm32, bm32_offs, resid, opts=None):
     return None
 
 
@@ -299,8 +300,9 @@ def _(pts, cam_offs, F, n_scenes, max_n, bmin8, bmin8_offs, resid, opts=None):
                          mutates_args=("workspace", "row_ind", "col_ind", "status"))
 def lsap_solve_resid_out(dims: Tensor, ws_offs: Tensor, out_offs: Tensor, workspace: Tensor,
                          row_ind: Tensor, col_ind: Tensor, status: Tensor, bmin8: Tensor,
-                         bmin8_offs: Tensor, segs: Tensor, resid: Tensor, max_n: int, long_min: int,
-                         long_max: int, short_max: int, opts: Optional[List[int]] = None) -> None:
+                         bmin8_offs: Tensor, bm32: Tensor, bm32_offs: Tensor, segs: Tensor,
+                         resid: Tensor, max_n: int, long_min: int, long_max: int, short_max: int,
+                         opts: Optional[List[int]] = None) -> None:
     """The assignment of every flattened cube of a triplet_minima batch, from
     its 8-row minima and pair residuals (mvm_lsap_solve_resid, ABI 7)."""
     dev = dims.device
@@ -310,20 +312,21 @@ def lsap_solve_resid_out(dims: Tensor, ws_offs: Tensor, out_offs: Tensor, worksp
                      (out_offs, "out_offs", torch.int64), (workspace, "workspace", torch.uint8),
                      (row_ind, "row_ind", torch.int64), (col_ind, "col_ind", torch.int64),
                      (status, "status", torch.int32), (bmin8, "bmin8", torch.int16),
-                     (bmin8_offs, "bmin8_offs", torch.int64), (segs, "segs", torch.int64),
+                     (bmin8_offs, "bmin8_offs", torch.int64), (bm32, "bm32", torch.int32),
+                     (bm32_offs, "bm32_offs", torch.int64), (segs, "segs", torch.int64),
                      (resid, "resid", torch.uint8)):
         _require(t, n, dt, dev)
     st = _native.load().mvm_lsap_solve_resid(_p(dims), status.numel(), _p(ws_offs), _p(out_offs),
                                              _p(workspace), workspace.numel(), _p(row_ind), _p(col_ind),
                                              _p(status), long_min, long_max, short_max, _p(bmin8),
-                                             _p(bmin8_offs), _p(segs), _p(resid), max_n, _opts_ref(opts),
-                                             _stream(dims))
+                                             _p(bmin8_offs), _p(bm32), _p(bm32_offs), _p(segs), _p(resid),
+                                             max_n, _opts_ref(opts), _stream(dims))
     _native.check("mvm_lsap_solve_resid", st)
 
 
 @lsap_solve_resid_out.register_fake
-def _(dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, bmin8, bmin8_offs, segs, resid,
-      max_n, long_min, long_max, short_max, opts=None):
+def _(dims, ws_offs, out_offs, workspace, row_ind, col_ind, status, bmin8, bmin8_offs, bm32, bm32_offs,
+      segs, resid, max_n, long_min, long_max, short_max, opts=None):
     return None
 
 
@@ -608,7 +611,14 @@ class TripletPlan:
         np.cumsum((counts[:, 0] * ((counts[:, 1] + 7) // 8) * counts[:, 2] + 3) // 4 * 4, out=bm8[1:])
         self.bmin8_offs_host = bm8
         self.n_bmin8 = int(bm8[-1])
-        self.bmin8_offs, self.segs = _h2d_int64([bm8, np.ascontiguousarray(counts[:, 1])], self.device)
+        # the cube-free path's 32-column block minima (mvm_triplet_minima): per
+        # scene P rows of ceil(M/32) * roundup(N, 16) uint32
+        b32 = np.zeros(n_scenes + 1, np.int64)
+        np.cumsum(counts[:, 2] * ((counts[:, 1] + 31) // 32) * ((counts[:, 0] + 15) // 16 * 16), out=b32[1:])
+        self.bm32_offs_host = b32
+        self.n_bm32 = int(b32[-1])
+        self.bmin8_offs, self.segs, self.bm32_offs = _h2d_int64(
+            [bm8, np.ascontiguousarray(counts[:, 1]), b32], self.device)
         self.workspace = torch.empty(max(self.workspace_bytes, 16), dtype=torch.uint8,
                                      device=self.device)
 
@@ -640,18 +650,23 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
 
 
 def triplet_minima(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
-                   bmin8: Optional[Tensor] = None, options: Optional[dict] = None):
+                   bmin8: Optional[Tensor] = None, bm32: Optional[Tensor] = None,
+                   options: Optional[dict] = None):
     """Cube-free input of the assignment (mvm_triplet_minima, ABI 7): the
     cube's 8-row minima (int16 [plan.n_bmin8], the same bits
-    ``triplet_cost_argmin(..., bmin8=)`` writes) and every scene's fp64 pair
-    residuals, written into ``plan.workspace`` (which the default cube kernels
-    do not use; a later cube launch on the plan with the workspace kernel
-    would overwrite them).  -> bmin8.  Views of at most 256 detections."""
+    ``triplet_cost_argmin(..., bmin8=)`` writes), the assignment's 32-column
+    block minima (int32 [plan.n_bm32]) and every scene's fp64 pair residuals,
+    written into ``plan.workspace`` (which the default cube kernels do not
+    use; a later cube launch on the plan with the workspace kernel would
+    overwrite them).  -> (bmin8, bm32).  Views of at most 256 detections."""
     if bmin8 is None:
         bmin8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=pts.device)
+    if bm32 is None:
+        bm32 = torch.empty(max(plan.n_bm32, 4), dtype=torch.int32, device=pts.device)
     torch.ops.mvmatch.triplet_minima_out(pts, cam_offs, F, plan.n_scenes, plan.max_n, bmin8,
-                                         plan.bmin8_offs, plan.workspace, _opts_list(options))
-    return bmin8
+                                         plan.bmin8_offs, bm32, plan.bm32_offs, plan.workspace,
+                                         _opts_list(options))
+    return bmin8, bm32
 
 
 def sparse_class_bounds() -> Tuple[int, int, int]:
@@ -781,23 +796,26 @@ def lsap_sparse_stats(plan: LsapPlan, min_cols: Optional[int] = None) -> np.ndar
     return out
 
 
-def linear_sum_assignment_resid(plan: LsapPlan, tplan: TripletPlan, bmin8: Tensor, *,
+def linear_sum_assignment_resid(plan: LsapPlan, tplan: TripletPlan, minima, *,
                                 options: Optional[dict] = None):
     """linear_sum_assignment_batched of every flattened (N*M, P) cube of a
     ``triplet_minima(..., tplan)`` batch without the cubes (mvm_lsap_solve_resid):
-    the same result (scipy's).  ``plan`` = LsapPlan(N*M, P, resid=True).
+    the same result (scipy's).  ``plan`` = LsapPlan(N*M, P, resid=True);
+    ``minima`` = what triplet_minima returned (bmin8, bm32).
     -> (row_ind, col_ind, status) as linear_sum_assignment_batched; status 4:
     a problem outside the candidate-list class (cube_free_scenes)."""
     if not plan.resid:
         raise ValueError("linear_sum_assignment_resid needs LsapPlan(..., resid=True)")
+    bmin8, bm32 = minima                  # what triplet_minima returned
     dev = bmin8.device
     row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)
     torch.ops.mvmatch.lsap_solve_resid_out(plan.dims, plan.ws_offs, plan.out_offs, plan.workspace,
-                                           row_ind, col_ind, status, bmin8, tplan.bmin8_offs,
-                                           tplan.segs, tplan.workspace, tplan.max_n, plan.long_min,
-                                           plan.long_max, plan.short_max, _opts_list(options))
+                                           row_ind, col_ind, status, bmin8, tplan.bmin8_offs, bm32,
+                                           tplan.bm32_offs, tplan.segs, tplan.workspace, tplan.max_n,
+                                           plan.long_min, plan.long_max, plan.short_max,
+                                           _opts_list(options))
     return row_ind[:plan.n_out], col_ind[:plan.n_out], status
 
 

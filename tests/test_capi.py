@@ -234,8 +234,9 @@ def test_lsap_plan_resid_sizes(lib):
     assert out.tolist() == [0, 256, 320, 360, 360, 384]
     sizes = np.diff(ws)
     assert sizes[3] == 0                              # an empty problem reserves nothing
-    # a 256^3 scene: its candidate lists and block minima, no transposed cost
-    assert 2e6 < sizes[0] < 3e6
+    # a 256^3 scene: its candidate lists only (the block minima come from
+    # mvm_triplet_minima; no transposed cost)
+    assert 2e5 < sizes[0] < 4e5
     # the dense plan reserves the transposed cost for the same problem
     ws2 = np.zeros(6, np.int64)
     lib.mvm_lsap_plan_ex(5, rows.ctypes.data, cols.ctypes.data, 0, ws2.ctypes.data, out.ctypes.data)
@@ -251,8 +252,8 @@ def test_lsap_solve_resid_validation(lib):
     before anything is launched (there is no cost for another class to read)."""
     def call(long_min, long_max, short_max, max_n=256, n=3):
         return lib.mvm_lsap_solve_resid(FAKE, n, FAKE, FAKE, FAKE, 1 << 20, FAKE, FAKE, FAKE,
-                                        long_min, long_max, short_max, FAKE, FAKE, FAKE, FAKE, max_n,
-                                        None, None)
+                                        long_min, long_max, short_max, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE,
+                                        max_n, None, None)
     assert call(600, 65536, 256) == 1
     assert b"candidate-list class" in lib.mvm_last_error_string()
     assert call(4096, 70000, 256) == 1
@@ -260,17 +261,19 @@ def test_lsap_solve_resid_validation(lib):
     assert call(4096, 65536, 256, max_n=300) == 2          # views of more than 256
     assert call(4096, 65536, 256, n=0) == 0                # nothing to solve
     assert lib.mvm_lsap_solve_resid(None, 3, FAKE, FAKE, FAKE, 0, FAKE, FAKE, FAKE, 4096, 65536, 256,
-                                    FAKE, FAKE, FAKE, FAKE, 256, None, None) == 1
+                                    FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, 256, None, None) == 1
 
 
 def test_triplet_minima_validation(lib):
     need = lib.mvm_triplet_workspace_bytes(10, 200)
-    args = lambda max_n, nbytes, resid=FAKE: (FAKE, FAKE, FAKE, 10, max_n, FAKE, FAKE, resid, nbytes,
-                                              None, None)
+    args = lambda max_n, nbytes, resid=FAKE: (FAKE, FAKE, FAKE, 10, max_n, FAKE, FAKE, FAKE, FAKE, resid,
+                                              nbytes, None, None)
     assert lib.mvm_triplet_minima(*args(300, 1 << 40)) == 2          # views of more than 256
     assert lib.mvm_triplet_minima(*args(200, need - 8)) == 3         # workspace too small
     assert lib.mvm_triplet_minima(*args(200, need, ctypes.c_void_p(0x1008))) == 1   # misaligned
     assert lib.mvm_triplet_minima(*args(200, need, None)) == 1       # null pointer
-    assert lib.mvm_triplet_minima(None, None, None, 0, 0, None, None, None, 0, None, None) == 0
+    assert lib.mvm_triplet_minima(None, None, None, 0, 0, None, None, None, None, None, 0, None, None) == 0
+    assert lib.mvm_triplet_minima(FAKE, FAKE, FAKE, 10, 200, FAKE, FAKE, ctypes.c_void_p(0x1004), FAKE,
+                                  FAKE, need, None, None) == 1      # misaligned block minima
     assert lib.mvm_select_triangulate_resid(None, 10, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, 3, 30.0,
                                             FAKE, FAKE, FAKE, FAKE, None) == 1

@@ -44,9 +44,23 @@ def _minima(cuda, counts, seed, options=None, **kw):
     t = lambda a: torch.from_numpy(a).to(cuda)
     P, C, FF = t(pts), t(co), t(F)
     bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int16, device=cuda)
+    bm32 = torch.full((max(plan.n_bm32, 4),), 0x5A5A5A5A, dtype=torch.int32, device=cuda)
     plan.workspace.fill_(0xFF)                       # NaN everywhere the kernel does not write
-    ops.triplet_minima(P, C, FF, plan, bmin8=bm8, options=options)
-    return plan, bm8, (pts, F, co), (P, C, FF)
+    minima = ops.triplet_minima(P, C, FF, plan, bmin8=bm8, bm32=bm32, options=options)
+    return plan, minima, (pts, F, co), (P, C, FF)
+
+
+def _want_bm32(keys: np.ndarray, N: int, M: int, P: int) -> np.ndarray:
+    """The block minima mvm_triplet_minima documents, from a scene's 8-row
+    minima (uint16 [N, ceil(M/8), P]): uint32 [P, ceil(M/32), roundup(N, 16)]."""
+    g8, bps, npad = (M + 7) // 8, (M + 31) // 32, (N + 15) // 16 * 16
+    pad = np.full((N, bps * 4, P), 0xFFFF, np.uint32)
+    pad[:, :g8] = keys
+    h = pad.reshape(N, bps, 4, P).min(axis=2)                         # [N, bps, P]
+    up = np.minimum((h << np.uint32(16)) | np.uint32(0xFFFF), np.uint32(0xFF800000))
+    out = np.full((P, bps, npad), 0xFFFFFFFF, np.uint32)
+    out[:, :, :N] = up.transpose(2, 1, 0)
+    return out
 
 
 MINIMA_BATCHES = {
@@ -58,15 +72,16 @@ MINIMA_BATCHES = {
 
 
 @pytest.mark.parametrize("batch", sorted(MINIMA_BATCHES))
-@pytest.mark.parametrize("rows", [0, 32])
-def test_minima_equal_cube_kernel_and_oracle(cuda, batch, rows):
-    """rows: i rows per chunk (mvm_options.cube_tile_rows; 0 = 16)"""
+def test_minima_equal_cube_kernel_and_oracle(cuda, batch):
+    """The 8-row minima (vs the cube kernel's and the oracle cube's), the
+    32-column block minima (vs their definition over the oracle's 8-row
+    minima, padding rows included) and the fp64 residuals (vs the oracle's)."""
     from bpc_baseline_amd import ops
     from oracle import oracle as O
     counts = MINIMA_BATCHES[batch]
-    plan, bm8, (pts, F, co), (P, C, FF) = _minima(cuda, counts, 5,
-                                                  options={"cube_tile_rows": rows} if rows else None)
+    plan, (bm8, bm32), (pts, F, co), (P, C, FF) = _minima(cuda, counts, 5)
     got = bm8.cpu().numpy().view(np.uint16)
+    got32 = bm32.cpu().numpy().view(np.uint32)
     # the cube kernel's own minima on the same batch
     ref8 = torch.full_like(bm8, -1)
     cube, _, _ = ops.triplet_cost_argmin(P, C, FF, plan, bmin8=ref8)
@@ -84,37 +99,42 @@ def test_minima_equal_cube_kernel_and_oracle(cuda, batch, rows):
         assert np.array_equal(got[o:o + n8], want_dev[o:o + n8]), (batch, s, "vs cube kernel")
         cs = oc[plan.cube_offs_host[s]:plan.cube_offs_host[s + 1]].reshape(N, M, Pn)
         assert np.array_equal(got[o:o + n8], O.bmin8_keys(cs).reshape(-1)), (batch, s, "vs oracle")
+        o32 = plan.bm32_offs_host[s]
+        want32 = _want_bm32(O.bmin8_keys(cs), N, M, Pn).reshape(-1)
+        assert np.array_equal(got32[o32:o32 + want32.size], want32), (batch, s, "block minima")
         for m, (a, b) in enumerate(((N, M), (Pn, N), (Pn, M))):
             g, w = resid[s, m, :a, :b], want_r[s, m, :a, :b]
             assert np.array_equal(g.view(np.int64), w.view(np.int64)), (batch, s, m)
 
 
-@pytest.mark.parametrize("rows", [0, 32])
-def test_minima_nonfinite_chunks(cuda, rows):
-    """NaN centroids and a degenerate F: the chunks with non-finite or huge
+def test_minima_nonfinite_chunks(cuda):
+    """NaN centroids and a degenerate F: the rows with non-finite or huge
     residuals take the exact per-entry path (keys equal the oracle's)."""
     from oracle import oracle as O
     counts = [(40, 70, 50), (64, 64, 64), (30, 100, 17)]
-    opts = {"cube_tile_rows": rows} if rows else None
     for kw in ({"nan_scene": 1, "nan_view": 0}, {"nan_scene": 0, "nan_view": 1},
                {"nan_scene": 2, "nan_view": 2}, {"degenerate_scene": 1}):
-        plan, bm8, (pts, F, co), _ = _minima(cuda, counts, 9, options=opts, **kw)
+        plan, (bm8, bm32), (pts, F, co), _ = _minima(cuda, counts, 9, **kw)
         got = bm8.cpu().numpy().view(np.uint16)
+        got32 = bm32.cpu().numpy().view(np.uint32)
         oc = O.cube(pts, co, F, len(counts))[0]
         for s, (N, M, Pn) in enumerate(counts):
             o, n8 = plan.bmin8_offs_host[s], N * ((M + 7) // 8) * Pn
             cs = oc[plan.cube_offs_host[s]:plan.cube_offs_host[s + 1]].reshape(N, M, Pn)
             assert np.array_equal(got[o:o + n8], O.bmin8_keys(cs).reshape(-1)), (kw, s)
+            o32 = plan.bm32_offs_host[s]
+            want32 = _want_bm32(O.bmin8_keys(cs), N, M, Pn).reshape(-1)
+            assert np.array_equal(got32[o32:o32 + want32.size], want32), (kw, s, "block minima")
 
 
 def _assign_both(cuda, counts, seed, options=None, **kw):
     from bpc_baseline_amd import ops
-    plan, bm8, host, (P, C, FF) = _minima(cuda, counts, seed, **kw)
+    plan, minima, host, (P, C, FF) = _minima(cuda, counts, seed, **kw)
     c3 = plan.counts
     lres = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=cuda, resid=True)
-    r1, c1, s1 = ops.linear_sum_assignment_resid(lres, plan, bm8, options=options)
+    r1, c1, s1 = ops.linear_sum_assignment_resid(lres, plan, minima, options=options)
     # the cube form on the same batch
-    ref8 = torch.empty_like(bm8)
+    ref8 = torch.empty_like(minima[0])
     cube, _, _ = ops.triplet_cost_argmin(P, C, FF, plan, bmin8=ref8)
     lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=cuda)
     r0, c0, s0 = ops.linear_sum_assignment_batched(cube, plan.cube_offs[:-1].contiguous(), lplan,
@@ -175,10 +195,10 @@ def test_resid_select_equals_cube_select(cuda, threshold):
 def test_resid_nan_status(cuda, nan_view):
     from bpc_baseline_amd import ops
     counts = [(40, 160, 64)] * 3
-    plan, bm8, _, _ = _minima(cuda, counts, 4, nan_scene=1, nan_view=nan_view)
+    plan, minima, _, _ = _minima(cuda, counts, 4, nan_scene=1, nan_view=nan_view)
     c3 = plan.counts
     lres = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=cuda, resid=True)
-    _, _, st = ops.linear_sum_assignment_resid(lres, plan, bm8)
+    _, _, st = ops.linear_sum_assignment_resid(lres, plan, minima)
     assert list(st.cpu().numpy()) == [0, 1, 0]
 
 
@@ -188,13 +208,13 @@ def test_resid_bounds(cuda):
     such a problem gets status 4, the others are solved."""
     from bpc_baseline_amd import _native, ops
     counts = [(64, 64, 64), (20, 30, 40), (70, 70, 70)]      # scene 1: a 600 x 40 problem
-    plan, bm8, _, _ = _minima(cuda, counts, 6)
+    plan, minima, _, _ = _minima(cuda, counts, 6)
     c3 = plan.counts
     lres = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=cuda, resid=True)
     with pytest.raises(_native.MvmError, match="candidate-list class"):
-        ops.linear_sum_assignment_resid(lres, plan, bm8)
+        ops.linear_sum_assignment_resid(lres, plan, minima)
     lres.long_min = 4096                                      # a caller whose bounds are wrong
-    _, _, st = ops.linear_sum_assignment_resid(lres, plan, bm8)
+    _, _, st = ops.linear_sum_assignment_resid(lres, plan, minima)
     assert list(st.cpu().numpy()) == [0, 4, 0]
 
 

@@ -115,7 +115,7 @@ for case in args.cases.split(","):
         fn = lambda: ops.linear_sum_assignment_batched(cube, offs, lp, bmin8=(bm8, tp.bmin8_offs, tp.segs))
         costs_host = lambda s: cube[tp.cube_offs_host[s]:tp.cube_offs_host[s + 1]].cpu().numpy()
     else:
-        bm8 = ops.triplet_minima(P, C, F, tp)
+        bm8 = ops.triplet_minima(P, C, F, tp)           # (8-row minima, block minima)
         lp = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
         fn = lambda: ops.linear_sum_assignment_resid(lp, tp, bm8)
 
