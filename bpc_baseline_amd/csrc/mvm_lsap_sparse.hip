@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kSpNT) void sp_bmin8_reduce_kernel(LsapSparseArgs a
 
 // ---- 2. candidate lists --------------------------------------------------------
 
-template <typename CT>
+template <typename CT, bool EXT>
 __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32_t n) {
     using K = SpKey<CT>;
     using KT = typename K::T;
@@ -461,7 +461,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     const int S = (int)(tr ? Kd : R), L = (int)(tr ? R : Kd);
     const SpLayout y = lsap_sparse_layout(S, L, sizeof(CT), tr, a.bm32 != nullptr);
     unsigned char *ws = a.ws + a.ws_offs[p];
-    const bool ext = a.bm32 != nullptr && sizeof(CT) == 4;   // block minima from mvm_triplet_minima
+    constexpr bool ext = EXT;                              // block minima from mvm_triplet_minima (a.bm32)
     int32_t *lcol = reinterpret_cast<int32_t *>(ws + y.lcol);
     CT *lval = reinterpret_cast<CT *>(ws + y.lval);
     int32_t *ln = reinterpret_cast<int32_t *>(ws + y.ln);
@@ -472,32 +472,57 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     bool src_ok;
     const SpSrc<CT> src = sp_src<CT>(a, p, tr, S, L, seg0, src_ok);
     if (!src_ok || (ext && !seg0)) return;                 // sp_solve_kernel reports it
+    // block b = g * bps + jt (segment g, part jt); lane l holds b = l, l + 64,
+    // ... -- one part of 32 segments, so each lane minimum ranges over 32
+    // different long-side rows (theta is taken over the lane minima).  ext:
+    // the blocks sit in mvm_triplet_minima's order, part-major -- b at
+    // jt * npad + g of a row of bps * npad keys (segments padded to a multiple
+    // of 16 with kMax) -- and lane l holds the 32 keys at 32 l .. 32 l + 31
+    // (one part, or two, of 32 consecutive segments: the same spread, eight
+    // 16-byte loads)
     const int bps = (seg + kSpBlock - 1) / kSpBlock, nseg = L / seg;
-    // ext: block b = jt * npad + g (rows g >= nseg padding, 0xFFFFFFFF);
-    // else b = g * bps + jt
+    const int nb = nseg * bps;
     const int npad = ext ? (nseg + 15) & ~15 : nseg;
-    const int nb = npad * bps;
+    const int rowk = npad * bps;                           // keys per row in memory
     const float rbps = 1.0f / (float)bps, rnpad = 1.0f / (float)npad;
-    auto decode = [&](int b, int &jt) {                    // -> segment g, part jt
-        if (ext) {
-            int g;
-            jt = sp_div(b, npad, rnpad, g);
-            return g;
-        }
-        return sp_div(b, bps, rbps, jt);
+    auto decode = [&](int b, int &jt) { return sp_div(b, bps, rbps, jt); };   // -> g, jt
+    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    // the block (g * bps + jt) lane `lane` holds in its q-th key
+    auto block_of = [&](int q) {
+        if (!ext) return lane + 64 * q;
+        int g;
+        const int jt = sp_div(32 * lane + q, npad, rnpad, g);
+        return g * bps + jt;
     };
     const KT *bm = ext ? reinterpret_cast<const KT *>(a.bm32 + a.bm32_offs[p])
                        : reinterpret_cast<const KT *>(ws + y.bm);
     int bad = 0;                                           // ext: a NaN entry (key 0) in these rows
-    const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     for (int s = grp * (kSpNT / 64) + wave; s < S; s += kSpRowGroups * (kSpNT / 64)) {
         KT k[kQ];
+        // the row base wave-uniform (a scalar base + 32-bit lane offsets)
+        const KT *row = bm + (int64_t)__builtin_amdgcn_readfirstlane(s) * rowk;
+        if constexpr (!ext) {
 #pragma unroll
-        for (int q = 0; q < kQ; ++q) {
-            const int idx = lane + 64 * q;
-            k[q] = idx < nb ? bm[(int64_t)s * nb + idx] : K::kMax;
-            if (ext) bad |= !(k[q] >> (8 * sizeof(KT) - 1));   // a NaN's key: below every value's
+            for (int q = 0; q < kQ; ++q) {
+                const int idx = lane + 64 * q;
+                k[q] = idx < nb ? row[idx] : K::kMax;
+            }
+        } else {
+            static_assert(kQ == 32 && sizeof(KT) == 4, "ext: 32 keys of 4 bytes per lane");
+            const uint4 *r4 = reinterpret_cast<const uint4 *>(row) + 8 * lane;
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {                  // rowk is a multiple of 16
+                const uint4 w = 32 * lane + 4 * v < rowk ? r4[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                k[4 * v] = w.x;
+                k[4 * v + 1] = w.y;
+                k[4 * v + 2] = w.z;
+                k[4 * v + 3] = w.w;
+            }
         }
+        KT lm = k[0];                                      // this lane's smallest block key
+#pragma unroll
+        for (int q = 1; q < kQ; ++q) lm = k[q] < lm ? k[q] : lm;
+        if (ext) bad |= !(lm >> (8 * sizeof(KT) - 1));     // a NaN's key: below every value's
         KT thr = K::kMax;
         CT theta = (CT)INFINITY;
         if (nb > a.tb) {
@@ -505,9 +530,6 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             // blocks l, l + 64, ...), so >= tb blocks hold a cost <= theta;
             // a search over one value per lane (32 steps of one compare), where
             // the tb-th smallest block minimum itself took 32 compares per step
-            KT lm = k[0];
-#pragma unroll
-            for (int q = 1; q < kQ; ++q) lm = k[q] < lm ? k[q] : lm;
             KT lo = 0, hi = K::kMax;
             while (lo < hi) {
                 const KT mid = lo + (hi - lo) / 2;
@@ -525,16 +547,17 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         int ncand = 0;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {
-            const bool c = (k[q] & lowmask) <= thr && lane + 64 * q < nb;
+            // (ext: padding holds kMax, above every key of a block)
+            const bool c = (k[q] & lowmask) <= thr && (ext ? k[q] != K::kMax : lane + 64 * q < nb);
             const uint64_t m = __ballot(c);
             if (c) {
                 const int pos = ncand + sp_mbcnt(m);
                 if (pos < kSpLCap) {
                     if (groups8) {                          // the block index
-                        s_cand[wave][pos] = lane + 64 * q;
+                        s_cand[wave][pos] = block_of(q);
                     } else {                                // its first column | its width << 16
                         int jt;
-                        const int g = decode(lane + 64 * q, jt);
+                        const int g = decode(block_of(q), jt);
                         s_cand[wave][pos] = (g * seg + jt * kSpBlock) | (min(kSpBlock, seg - jt * kSpBlock) << 16);
                     }
                 }
@@ -559,7 +582,7 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                     int jt;
                     const int g = decode(s_cand[wave][idx], jt);
                     const int g8 = 4 * jt + u;
-                    if (g8 < bps8 && g < nseg) {            // (padding rows: never candidates)
+                    if (g8 < bps8) {
                         c = ((KT)B8[(int64_t)(g * bps8 + g8) * S + s] << 16) <= thr;
                         e = (g * seg + 8 * g8) | (min(8, seg - 8 * g8) << 16);
                     }
@@ -1081,7 +1104,10 @@ int sp_launch(const LsapSparseArgs &a0, int32_t n, int64_t long_max, hipStream_t
     if (!a.resid) sp_blockmin_kernel<CT><<<dim3((unsigned)(n * tpp)), dim3(kSpNT), 0, s>>>(a, n, tpp);
     if (a.bmin8 && !a.bm32)
         sp_bmin8_reduce_kernel<<<dim3((unsigned)(n * (kSpMaxBlocks / 64))), dim3(kSpNT), 0, s>>>(a, n);
-    sp_lists_kernel<CT><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
+    if (sizeof(CT) == 4 && a.bm32)                           // (a double problem has no bm32)
+        sp_lists_kernel<CT, sizeof(CT) == 4><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
+    else
+        sp_lists_kernel<CT, false><<<dim3((unsigned)(n * kSpRowGroups)), dim3(kSpNT), 0, s>>>(a, n);
     const int cap = a.s_cap;
     const int lw = (int)(((lmax + 63) / 64) * 2);            // even: the f64 arrays stay 8-aligned
     const size_t lds = sp_solve_lds_bytes(lw, cap);
