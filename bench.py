@@ -537,8 +537,11 @@ def run_match(args, env, wl, kernel_options):
         raise SystemExit(3)
 
 
+FREE_LSAP_INPUT = "bmin8"      # the cube-free chain's default block source (--lsap-input auto)
+
+
 def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free", cpu_seconds=0.0,
-               n_chunks_req=1, lsap_input="bmin8"):
+               n_chunks_req=1, lsap_input="auto"):
     """What ``match_objects`` returns, at C2 scale (the ``c2match`` workload).
 
     A step is every scene of this rank through the device chain of
@@ -561,6 +564,10 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
     from bpc_baseline_amd.inference.utils.camera_utils import projection_matrices
     dev, world = env.device, env.world
     free = cube_mode == "free"
+    if lsap_input == "auto":
+        lsap_input = FREE_LSAP_INPUT if free else "bmin8"
+    if (free and lsap_input == "cost") or (not free and lsap_input == "blocks"):
+        raise SystemExit(f"c2match: --lsap-input {lsap_input} does not apply to --cube {cube_mode}")
     if args.scaling == "weak":
         first, n_local = env.rank * wl["n_scenes"], wl["n_scenes"]
     else:
@@ -598,7 +605,9 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                 raise SystemExit("c2match --cube free: a scene outside the candidate-list class")
             ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
             ch["cube"] = None
-            ch["bm8"] = torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+            # --lsap-input blocks: no 8-row minima (the lists gather whole blocks)
+            ch["bm8"] = torch.empty(max(tp.n_bmin8, 1) if lsap_input == "bmin8" else 0,
+                                    dtype=torch.int16, device=dev)
             ch["bm32"] = torch.empty(max(tp.n_bm32, 4), dtype=torch.int32, device=dev)
         else:
             ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
@@ -706,11 +715,18 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
             n3 = tuple(int(x) for x in ch["tplan"].counts[sl])
             tp = ch["tplan"]
             if free:
-                # the 8-row minima and the pair residuals the assignment read
-                o8 = int(tp.bmin8_offs_host[sl])
-                n8 = n3[0] * ((n3[1] + 7) // 8) * n3[2]
-                keys = ch["bm8"][o8:o8 + n8].cpu().numpy().view(np.uint16)
-                keys_ok = np.array_equal(keys, O.bmin8_keys(rc.reshape(n3)).reshape(-1))
+                # the 8-row minima (when written), the block minima and the
+                # pair residuals the assignment read
+                want8 = O.bmin8_keys(rc.reshape(n3))
+                keys_ok = True
+                if ch["bm8"].numel():
+                    o8 = int(tp.bmin8_offs_host[sl])
+                    keys = ch["bm8"][o8:o8 + want8.size].cpu().numpy().view(np.uint16)
+                    keys_ok = np.array_equal(keys, want8.reshape(-1))
+                want32 = O.bm32_keys(want8, *n3).reshape(-1)
+                o32 = int(tp.bm32_offs_host[sl])
+                keys_ok &= np.array_equal(ch["bm32"][o32:o32 + want32.size].cpu().numpy().view(np.uint32),
+                                          want32)
                 co1 = batch.cam_offs[3 * s:3 * s + 4]
                 want_r = O.residuals(batch.pts[int(co1[0]):int(co1[3])], co1 - co1[0],
                                      batch.F[3 * s:3 * s + 3], 1, tp.max_n)[0]
@@ -742,7 +758,8 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
             parity_ok &= bool(cube_ok and lsap_ok and match_ok and cost_ok and x_ok)
             d = {"scene": first + s}
             if free:
-                d.update({"bmin8_bit_exact": bool(keys_ok), "residuals_bit_exact": bool(resid_ok)})
+                d.update({("bmin8_bm32_bit_exact" if ch["bm8"].numel() else "bm32_bit_exact"): bool(keys_ok),
+                          "residuals_bit_exact": bool(resid_ok)})
             else:
                 d["cube_bit_exact"] = bool(cube_ok)
             d.update({"assignment_equal": bool(lsap_ok), "matches": k,
@@ -762,7 +779,8 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
         # the minima pass: centroids + F in; 8-row minima, block minima and
         # fp64 residuals out
         n_bm32 = sum(ch["tplan"].n_bm32 for ch in chunks)
-        first_bytes = (16.0 * counts.sum() + 3 * 72.0 * len(N) + 2.0 * float(n_bmin8)
+        n8w = n_bmin8 if lsap_input == "bmin8" else 0
+        first_bytes = (16.0 * counts.sum() + 3 * 72.0 * len(N) + 2.0 * float(n8w)
                        + 4.0 * float(n_bm32) + 8.0 * float((N * M + P * N + P * M).sum()))
         lsap_bytes = 4.0 * float(n_bm32)
         first_kernel = "triplet_minima_kernel"
@@ -793,17 +811,20 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                           f"x{threads}) + scipy.optimize.linear_sum_assignment (the reference's "
                           "own call, one core) + threshold/sort + numpy SVD per match, on "
                           f"{cpu_model()}")}
-    # the minima pass is fp64-VALU bound: per triple two fp64 adds and one fp64
-    # min (its algorithmic operations), against the MI355X fp64 vector peak
+    # the minima pass's arithmetic floor: per triple one float32 add (e12 + e23;
+    # + e13 and the third run once per 8 triples) and half a v_min3_f32 (two
+    # of the group's seven mins), at the VALU's 2-cycle wave64 issue: 78.6e12
+    # lane-instructions/s (MI355X_MICROARCH.md); the exact fp64 recheck of
+    # the groups near a 16-bit carry is not counted
     valu = None
     if free and cube_ms > 0:
-        ops_per_s = 3.0 * triples / (cube_ms * 1e-3)
-        valu = {"bound": "fp64 valu", "kernel": "triplet_minima_kernel",
-                "achieved": ops_per_s / 1e12, "peak": 78.6, "unit": "TFLOP/s",
-                "frac": ops_per_s / 1e12 / 78.6, "ops_per_triple": 3,
-                "note": ("algorithmic fp64 operations (two adds and one min per triple; the third "
-                         "and the cast run once per 8 triples and are not counted) over the stage's "
-                         "HIP-event time, against the fp64 vector peak (MI355X_MICROARCH.md)")}
+        per_s = 1.5 * triples / (cube_ms * 1e-3)
+        valu = {"bound": "f32 valu issue", "kernel": "triplet_minima_kernel",
+                "achieved": per_s / 1e12, "peak": 78.6, "unit": "T lane-instr/s",
+                "frac": per_s / 1e12 / 78.6, "instr_per_triple": 1.5,
+                "note": ("algorithmic VALU lane-instructions (one v_add_f32, half a v_min3_f32 per "
+                         "triple) over the stage's HIP-event time, against 256 CUs x 4 SIMDs x 32 "
+                         "lanes x 2.4 GHz (MI355X_MICROARCH.md: wave64 issue in 2 cycles)")}
     line = {
         "metric": "captures matched/sec (cost cube + scipy-identical assignment + select/DLT)",
         "value": value, "unit": "captures/s", "n_gpus": world, "steps": steps,
@@ -816,7 +837,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                    "cube": ("free: 8-row minima + fp64 pair residuals, entries recomputed where read "
                             "(match_captures keep_cube=False)" if free else
                             "keep: the cost cubes written and read (keep_cube=True)"),
-                   "lsap_input": "bmin8" if free else lsap_input,
+                   "lsap_input": lsap_input,
                    "launch": (f"eager op calls, {n_chunks} chunks of scenes: cubes on the launch "
                               "stream, each chunk's assignment + select on a second stream once "
                               "its cube is written" if n_chunks > 1 else "eager op calls, serial"),
@@ -904,9 +925,11 @@ def main():
                     help="auto (default): the c3 workload on one GPU also measures c2match "
                          "(cube-free) after its own line's parity and nests it in the line as "
                          "\"c2match\"; off: not")
-    ap.add_argument("--lsap-input", choices=["bmin8", "cost"], default="bmin8",
-                    help="c2match: the assignment's block minima from the cube kernel's 8-row "
-                         "minima (default) or from reading the cost cubes again")
+    ap.add_argument("--lsap-input", choices=["auto", "bmin8", "blocks", "cost"], default="auto",
+                    help="c2match: the assignment's candidate blocks refined by the 8-row minima "
+                         "(bmin8), whole 32-column blocks from the block minima alone (blocks: "
+                         "--cube free only; no 8-row minima written) or the cost cubes read again "
+                         "(cost: --cube keep only); auto: FREE_LSAP_INPUT / bmin8")
     ap.add_argument("--dry-run", action="store_true",
                     help="start the ranks and the process group (gloo, host only) and print the "
                          "world each rank joined; no GPU work (tests the launcher on a CPU host)")

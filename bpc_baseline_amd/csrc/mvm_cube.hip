@@ -1511,6 +1511,15 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
 // [IB][32] tile go through LDS.  The e23 column (32 j) sits in the thread's
 // registers for the whole scene.  Workgroups of block 0 write e13T, every
 // workgroup its e23T rows and e12 columns.
+// the approximate minima (triplet_minima_kernel): residuals up to 2^64 (their
+// float32 images and sums finite), the lower 16 bits of a float32 cost at
+// least kApproxMargin from a carry either way, costs >= 2^-100 (normal
+// float32 throughout)
+constexpr double kApproxResidual = 0x1p64;
+constexpr uint32_t kApproxMargin = 16;
+constexpr uint32_t kApproxTiny = 0x0D800000u;   // the bits of 2^-100
+constexpr float kThirdF = 1.0f / 3.0f;
+
 struct MinimaArgs {
     const double *pts;
     const int64_t *cam_offs;
@@ -1531,8 +1540,11 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     constexpr int kJ = 32;                     // j per workgroup: four 8-row groups
     static_assert(IB == 16, "the chunk's block minima leave as one 64-byte run per k");
     __shared__ __attribute__((aligned(16))) double s12[IB][kJ];
-    __shared__ LineRec s_r13[IB], s_r12[IB], s_c12[kJ], s_r23[kJ];
-    __shared__ double s_p0[IB][2], s_p1[kJ][2];
+    __shared__ __attribute__((aligned(16))) float s12f[IB][kJ];
+    // the chunk's row lines, double-buffered: wave 0 writes chunk c + 1's
+    // while the other waves may still read chunk c's
+    __shared__ LineRec s_r13[2][IB], s_r12[2][IB], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[2][IB][2], s_p1[kJ][2];
     __shared__ __attribute__((aligned(16))) uint32_t s_bm[IB][kThreads];   // the chunk's block minima
 
     const int t = threadIdx.x;
@@ -1559,7 +1571,7 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     double *E13T = E12 + (int64_t)args.max_n * ld;
     double *E23T = E13T + (int64_t)args.max_n * ld;
     const int g8 = (M + 7) / 8;
-    uint16_t *B8 = args.bmin8 + args.bmin8_offs[s];
+    uint16_t *B8 = args.bmin8 ? args.bmin8 + args.bmin8_offs[s] : nullptr;   // optional
     const int npad = (N + 15) & ~15;
     const int nbk = ((M + 31) / 32) * npad;
     uint32_t *BM = args.bm32 + args.bm32_offs[s] + (int64_t)k * nbk + (int64_t)jb * npad;
@@ -1606,33 +1618,39 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                           line_dist(row.l0, row.l1, row.l2, cx, cy));   // :28
         return pair_e(col, row, rx, ry, cx, cy);
     };
-    // e23[j][k] of the block's 32 j; rows past the view hold +inf, so they
-    // never decide a group's minimum (their sums are +inf, or NaN where a
-    // valid row of the same k is NaN too)
-    bool tame = true;
-    double a23[kJ];
-#pragma unroll
-    for (int jj = 0; jj < kJ; ++jj) {
-        a23[jj] = jj >= nj ? (double)INFINITY
-                  : kv      ? pair(!deg_fixed, c23, s_r23[jj], s_p1[jj][0], s_p1[jj][1], kx, ky)
-                            : 0.0;
-        tame &= jj >= nj || a23[jj] <= kTameResidual;
-    }
-    if (kv) {                                    // e23T row k: the block's j (256 contiguous bytes)
+    // e23[j][k] of the block's 32 j, in float32 for the approximate minima
+    // (rows past the view +inf: never a group's minimum); the fp64 values go
+    // to e23T and are recomputed where an exact minimum is needed
+    auto e23_at = [&](int jj) {
+        return jj >= nj ? (double)INFINITY
+               : kv     ? pair(!deg_fixed, c23, s_r23[jj], s_p1[jj][0], s_p1[jj][1], kx, ky)
+                        : 0.0;
+    };
+    bool near = true;                            // every residual <= kApproxResidual
+    float f23[kJ];
+    {
         double *dst = E23T + (int64_t)k * ld + jw0;
-        if (nj == kJ) {
 #pragma unroll
-            for (int jj = 0; jj < kJ; jj += 2) *reinterpret_cast<f64x2 *>(dst + jj) = f64x2{a23[jj], a23[jj + 1]};
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < kJ; ++jj)
-                if (jj < nj) dst[jj] = a23[jj];
+        for (int jj = 0; jj < kJ; jj += 2) {
+            const double a0 = e23_at(jj), a1 = e23_at(jj + 1);
+            near &= (jj >= nj || a0 <= kApproxResidual) && (jj + 1 >= nj || a1 <= kApproxResidual);
+            f23[jj] = (float)a0;
+            f23[jj + 1] = (float)a1;
+            if (kv) {                            // e23T row k: the block's j (256 contiguous bytes)
+                if (nj == kJ) {
+                    *reinterpret_cast<f64x2 *>(dst + jj) = f64x2{a0, a1};
+                } else {
+                    if (jj < nj) dst[jj] = a0;
+                    if (jj + 1 < nj) dst[jj + 1] = a1;
+                }
+            }
         }
     }
 
     // ---- the scene's i rows, IB at a time --------------------------------------
     for (int i0 = 0; i0 < N; i0 += IB) {
         const int ni = min(IB, N - i0);
+        const int cb = (i0 / IB) & 1;            // this chunk's row-line buffer
         bool deg_rows = false;
         static_assert(IB <= kWave, "the chunk's row lines: one thread of wave 0 each");
         if (t < IB) {
@@ -1648,57 +1666,84 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                 b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
             }
             deg_rows = (a.deg != 0.0) || (b.deg != 0.0);
-            s_r13[t] = a;
-            s_r12[t] = b;
-            s_p0[t][0] = px;
-            s_p0[t][1] = py;
+            s_r13[cb][t] = a;
+            s_r12[cb][t] = b;
+            s_p0[cb][t][0] = px;
+            s_p0[cb][t][1] = py;
         }
         // (the barrier also puts every wave past the previous chunk's reads of
-        // s12: it must run whatever deg_fixed is -- no short circuit)
+        // s12 / s12f: it must run whatever deg_fixed is -- no short circuit)
         const bool deg_chunk = __syncthreads_or(deg_rows) != 0;
         const bool nd = !deg_fixed && !deg_chunk;
-        bool tame_c = tame;
+        bool near_c = near;
         for (int x = t; x < IB * kJ; x += kThreads) {
             const int r = x / kJ, jj = x % kJ;
             const bool v = r < ni && jj < nj;
-            const double e =
-                v ? pair(nd, s_c12[jj], s_r12[r], s_p0[r][0], s_p0[r][1], s_p1[jj][0], s_p1[jj][1]) : 0.0;
+            const double e = v ? pair(nd, s_c12[jj], s_r12[cb][r], s_p0[cb][r][0], s_p0[cb][r][1],
+                                      s_p1[jj][0], s_p1[jj][1])
+                               : 0.0;
             s12[r][jj] = e;
-            tame_c &= e <= kTameResidual;
+            s12f[r][jj] = (float)e;
+            near_c &= e <= kApproxResidual;
             if (v) E12[(int64_t)(i0 + r) * ld + jw0 + jj] = e;
         }
-        const bool chunk_fast = __syncthreads_and(tame_c) != 0;
+        const bool chunk_near = __syncthreads_and(near_c) != 0;
         for (int ii = 0; ii < ni; ++ii) {
             const int i = i0 + ii;
-            const double e13 = kv ? pair(nd, cl13, s_r13[ii], s_p0[ii][0], s_p0[ii][1], kx, ky) : 0.0;
+            const double e13 =
+                kv ? pair(nd, cl13, s_r13[cb][ii], s_p0[cb][ii][0], s_p0[cb][ii][1], kx, ky) : 0.0;
             if (jb == 0 && kv) E13T[(int64_t)k * ld + i] = e13;
-            // every sum of the wave's rows is finite (wave-uniform)
-            const bool fast = chunk_fast && __all(e13 <= kTameResidual);
+            // every residual of the wave's rows <= kApproxResidual (wave-uniform)
+            const bool fast = chunk_near && __all(e13 <= kApproxResidual);
             // the four groups' keys (a group past the view -- all its e23
             // +inf -- is computed and ignored below)
             uint32_t key[kJ / 8];
             if (fast) {
+                const float f13 = (float)e13;
 #pragma unroll
                 for (int g = 0; g < kJ / 8; ++g) {
-                    double sm[8];
+                    // float32 sums, each within 3 units of 2^-24 of the exact
+                    // (nonnegative) sum: their minimum, + e13 and / 3 lands
+                    // within 6 units in the last place of the float32 cost of
+                    // the exact minimum.  Its upper 16 bits are
+                    // the key's unless the lower 16 lie within kApproxMargin of
+                    // a carry, or the value is tiny (subnormal inputs): then
+                    // this lane's group is computed exactly below
+                    float v[8];
 #pragma unroll
-                    for (int r = 0; r < 8; r += 2) {
-                        const f64x2 w = *reinterpret_cast<const f64x2 *>(&s12[ii][8 * g + r]);
-                        sm[r] = (w.x + e13) + a23[8 * g + r];              // (e12 + e13) + e23, :81
-                        sm[r + 1] = (w.y + e13) + a23[8 * g + r + 1];
+                    for (int r = 0; r < 8; r += 4) {
+                        const f32x4 w = *reinterpret_cast<const f32x4 *>(&s12f[ii][8 * g + r]);
+                        v[r] = w.x + f23[8 * g + r];
+                        v[r + 1] = w.y + f23[8 * g + r + 1];
+                        v[r + 2] = w.z + f23[8 * g + r + 2];
+                        v[r + 3] = w.w + f23[8 * g + r + 3];
                     }
-                    // a tree: the same minimum (no NaN here), three dependent steps
-                    const double m = fmin(fmin(fmin(sm[0], sm[1]), fmin(sm[2], sm[3])),
-                                          fmin(fmin(sm[4], sm[5]), fmin(sm[6], sm[7])));
-                    key[g] = __float_as_uint((float)third_q(m)) | 0x80000000u;
+                    const float m = __builtin_fminf(
+                        __builtin_fminf(__builtin_fminf(v[0], v[1]), __builtin_fminf(v[2], v[3])),
+                        __builtin_fminf(__builtin_fminf(v[4], v[5]), __builtin_fminf(v[6], v[7])));
+                    const uint32_t b = __float_as_uint((m + f13) * kThirdF);
+                    const bool ok = !kv || 8 * g >= nj ||
+                                    ((b & 0xFFFFu) - kApproxMargin < 0x10000u - 2 * kApproxMargin &&
+                                     b >= kApproxTiny);
+                    key[g] = b | 0x80000000u;
+                    if (!ok) {                           // exact: eight fp64 sums
+                        double sm = (double)INFINITY;
+#pragma unroll 1
+                        for (int r = 0; r < 8; ++r) {
+                            const int jj = 8 * g + r;
+                            sm = fmin(sm, (s12[ii][jj] + e13) + e23_at(jj));   // (e12 + e13) + e23, :81
+                        }
+                        key[g] = __float_as_uint((float)third_q(sm)) | 0x80000000u;
+                    }
                 }
             } else {   // a huge / non-finite residual: every entry exactly
 #pragma unroll 1
                 for (int g = 0; g < kJ / 8; ++g) {
                     uint32_t kk = 0xFFFFFFFFu;
-#pragma unroll
+#pragma unroll 1
                     for (int r = 0; r < 8; ++r) {
-                        const double sum = (s12[ii][8 * g + r] + e13) + a23[8 * g + r];
+                        const int jj = 8 * g + r;
+                        const double sum = (s12[ii][jj] + e13) + e23_at(jj);
                         double qv = third_q(sum);
                         qv = third_ok(qv) ? qv : sum / 3.0;
                         kk = umin(kk, bm8_key((float)qv));
@@ -1712,7 +1757,7 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                 if (8 * g < nj) {                // uniform
                     const uint32_t h = key[g] >> 16;
                     hmin = umin(hmin, h);
-                    if (kv) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
+                    if (kv && B8) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
                 }
             }
             // sp_bmin8_reduce_kernel's upper bound of the block minimum
@@ -1824,8 +1869,8 @@ int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const
         return mvm_fail(MVM_ERR_UNSUPPORTED, "mvm_triplet_minima: views of at most %d detections "
                         "(%d given)", kChunk, (int)max_n);
     if (n_scenes == 0 || max_n == 0) return MVM_OK;
-    if (!pts_dev || !cam_offs_dev || !F_dev || !bmin8_dev || !bmin8_offs_dev || !bm32_dev ||
-        !bm32_offs_dev || !resid_dev)
+    if (!pts_dev || !cam_offs_dev || !F_dev || (bmin8_dev && !bmin8_offs_dev) || !bm32_dev ||
+        !bm32_offs_dev || !resid_dev)   // (the 8-row minima are optional)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     if (((uintptr_t)bm32_dev & 15) != 0)
         return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "bm32 not 16-byte aligned");

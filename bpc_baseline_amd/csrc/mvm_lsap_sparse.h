@@ -66,7 +66,7 @@ constexpr int kSpMaxBlocks = 2048;   // block minima per row (32 keys per wave l
 // problem p's blocks come from bmin8: the segment length (a cube's M), else 0
 // (blocks of 32 over the whole long side, from the cost itself)
 __host__ __device__ inline int lsap_sparse_seg(const LsapSparseArgs &a, int p, bool tr, int L) {
-    if (!a.bmin8 || !a.bmin8_offs || !a.segs || !tr) return 0;
+    if (((!a.bmin8 || !a.bmin8_offs) && !a.bm32) || !a.segs || !tr) return 0;   // 8-row or block minima
     const int64_t seg = a.segs[p];
     if (seg <= 0 || L % seg != 0) return 0;
     return (L / seg) * ((seg + 31) / 32) <= kSpMaxBlocks ? (int)seg : 0;

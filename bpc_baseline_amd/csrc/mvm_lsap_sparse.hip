@@ -1209,15 +1209,16 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
                             "all of the candidate-list class (long sides >= %d, > %d, <= %d; short sides "
                             "<= %d)", (long long)long_min, (long long)long_max, (long long)short_max, sp_lo,
                             wave_max, kSpMaxCols, kSpMaxShort);
-        if (!bmin8_dev || !bmin8_offs_dev || !bm32_dev || !bm32_offs_dev || !segs_dev || !resid_dev ||
-            !workspace_dev || !row_ind_dev || !col_ind_dev)
+        if ((bmin8_dev && !bmin8_offs_dev) || !bm32_dev || !bm32_offs_dev || !segs_dev || !resid_dev ||
+            !workspace_dev || !row_ind_dev || !col_ind_dev)   // (the 8-row minima are optional)
             return mvm_fail(MVM_ERR_INVALID_ARGUMENT, "null pointer");
     }
     (void)workspace_bytes;   // the per-problem regions come from mvm_lsap_plan_resid's offsets
     LsapSparseArgs sa{nullptr, nullptr, dims_dev, ws_offs_dev,
                       reinterpret_cast<unsigned char *>(workspace_dev), out_offs_dev, row_ind_dev,
                       col_ind_dev, status_dev, sp_lo > 0 ? sp_lo : 1, wave_max,
-                      (int32_t)(short_max < 1 ? 1 : short_max), bmin8_dev, bmin8_offs_dev, segs_dev,
+                      (int32_t)(short_max < 1 ? 1 : short_max), bmin8_dev,
+                      bmin8_dev ? bmin8_offs_dev : nullptr, segs_dev,
                       o.lsap_sparse_blocks ? o.lsap_sparse_blocks : kSpTB};
     const int ld = (max_n + 3) / 4 * 4;
     sa.resid = resid_dev;

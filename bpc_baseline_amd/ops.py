@@ -651,15 +651,19 @@ def triplet_cost_argmin(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletP
 
 def triplet_minima(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, *,
                    bmin8: Optional[Tensor] = None, bm32: Optional[Tensor] = None,
-                   options: Optional[dict] = None):
+                   with_bmin8: bool = True, options: Optional[dict] = None):
     """Cube-free input of the assignment (mvm_triplet_minima, ABI 7): the
     cube's 8-row minima (int16 [plan.n_bmin8], the same bits
     ``triplet_cost_argmin(..., bmin8=)`` writes), the assignment's 32-column
     block minima (int32 [plan.n_bm32]) and every scene's fp64 pair residuals,
     written into ``plan.workspace`` (which the default cube kernels do not
     use; a later cube launch on the plan with the workspace kernel would
-    overwrite them).  -> (bmin8, bm32).  Views of at most 256 detections."""
-    if bmin8 is None:
+    overwrite them).  -> (bmin8, bm32).  Views of at most 256 detections.
+    ``with_bmin8=False``: no 8-row minima (bmin8 an empty tensor; the
+    assignment then gathers whole 32-column candidate blocks)."""
+    if not with_bmin8:
+        bmin8 = torch.empty(0, dtype=torch.int16, device=pts.device)
+    elif bmin8 is None:
         bmin8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=pts.device)
     if bm32 is None:
         bm32 = torch.empty(max(plan.n_bm32, 4), dtype=torch.int32, device=pts.device)
@@ -806,8 +810,8 @@ def linear_sum_assignment_resid(plan: LsapPlan, tplan: TripletPlan, minima, *,
     a problem outside the candidate-list class (cube_free_scenes)."""
     if not plan.resid:
         raise ValueError("linear_sum_assignment_resid needs LsapPlan(..., resid=True)")
-    bmin8, bm32 = minima                  # what triplet_minima returned
-    dev = bmin8.device
+    bmin8, bm32 = minima                  # what triplet_minima returned (bmin8 may be empty)
+    dev = bm32.device
     row_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     col_ind = torch.empty(max(plan.n_out, 1), dtype=torch.int64, device=dev)
     status = torch.empty(plan.n, dtype=torch.int32, device=dev)

@@ -51,16 +51,8 @@ def _minima(cuda, counts, seed, options=None, **kw):
 
 
 def _want_bm32(keys: np.ndarray, N: int, M: int, P: int) -> np.ndarray:
-    """The block minima mvm_triplet_minima documents, from a scene's 8-row
-    minima (uint16 [N, ceil(M/8), P]): uint32 [P, ceil(M/32), roundup(N, 16)]."""
-    g8, bps, npad = (M + 7) // 8, (M + 31) // 32, (N + 15) // 16 * 16
-    pad = np.full((N, bps * 4, P), 0xFFFF, np.uint32)
-    pad[:, :g8] = keys
-    h = pad.reshape(N, bps, 4, P).min(axis=2)                         # [N, bps, P]
-    up = np.minimum((h << np.uint32(16)) | np.uint32(0xFFFF), np.uint32(0xFF800000))
-    out = np.full((P, bps, npad), 0xFFFFFFFF, np.uint32)
-    out[:, :, :N] = up.transpose(2, 1, 0)
-    return out
+    from oracle import oracle as O
+    return O.bm32_keys(keys, N, M, P)
 
 
 MINIMA_BATCHES = {
@@ -167,6 +159,32 @@ def test_resid_assignment_equals_cube_and_scipy(cuda, counts, blocks):
             continue
         rr, cc = scipy_lsa(c[plan.cube_offs_host[s]:plan.cube_offs_host[s + 1]].reshape(N * M, P))
         assert np.array_equal(r1[o[s]:o[s + 1]], rr) and np.array_equal(c1[o[s]:o[s + 1]], cc), (N, M, P)
+
+
+@pytest.mark.parametrize("counts", ASSIGN_BATCHES)
+@pytest.mark.parametrize("blocks", [0, 1])
+def test_resid_assignment_without_bmin8(cuda, counts, blocks):
+    """No 8-row minima (with_bmin8=False): the block minima and residuals are
+    the same bits, and the lists, gathering whole 32-column blocks, give the
+    same assignment as the cube form."""
+    from bpc_baseline_amd import ops
+    opts = {"lsap_sparse_blocks": blocks} if blocks else None
+    plan, lres, lplan, cube, _, (r0, c0, s0), _, (P, C, FF) = _assign_both(cuda, counts, 11, opts)
+    bm32_with = ops.triplet_minima(P, C, FF, plan)[1].clone()
+    ws_with = plan.workspace.clone()
+    plan.workspace.fill_(0xFF)
+    bm8, bm32 = ops.triplet_minima(P, C, FF, plan, with_bmin8=False)
+    assert bm8.numel() == 0
+    assert torch.equal(bm32[:plan.n_bm32], bm32_with[:plan.n_bm32])
+    for s, (N, M, Pn) in enumerate(counts):      # the residuals the kernel writes, bit for bit
+        stride = 3 * plan.max_n * ((plan.max_n + 3) // 4 * 4) * 8
+        a = ws_with[s * stride:(s + 1) * stride].view(torch.float64).view(3, plan.max_n, -1)
+        b = plan.workspace[s * stride:(s + 1) * stride].view(torch.float64).view(3, plan.max_n, -1)
+        for m, (x, y) in enumerate(((N, M), (Pn, N), (Pn, M))):
+            assert torch.equal(a[m, :x, :y].view(torch.int64), b[m, :x, :y].view(torch.int64)), (s, m)
+    r1, c1, s1 = ops.linear_sum_assignment_resid(lres, plan, (bm8, bm32), options=opts)
+    assert (s1.cpu().numpy() == 0).all() and (s0.cpu().numpy() == 0).all()
+    assert torch.equal(r1, r0) and torch.equal(c1, c0)
 
 
 @pytest.mark.parametrize("threshold", [30.0, 200.0, float("inf")])
