@@ -1516,7 +1516,7 @@ __global__ __launch_bounds__(kThreads) void bmin8_from_cube_kernel(const int64_t
 // least kApproxMargin from a carry either way, costs >= 2^-100 (normal
 // float32 throughout)
 constexpr double kApproxResidual = 0x1p64;
-constexpr uint32_t kApproxMargin = 16;
+constexpr uint32_t kApproxMargin = 8;
 constexpr uint32_t kApproxTiny = 0x0D800000u;   // the bits of 2^-100
 constexpr float kThirdF = 1.0f / 3.0f;
 
@@ -1541,11 +1541,12 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     static_assert(IB == 16, "the chunk's block minima leave as one 64-byte run per k");
     __shared__ __attribute__((aligned(16))) double s12[IB][kJ];
     __shared__ __attribute__((aligned(16))) float s12f[IB][kJ];
-    // the chunk's row lines, double-buffered: wave 0 writes chunk c + 1's
-    // while the other waves may still read chunk c's
-    __shared__ LineRec s_r13[2][IB], s_r12[2][IB], s_c12[kJ], s_r23[kJ];
-    __shared__ double s_p0[2][IB][2], s_p1[kJ][2];
-    __shared__ __attribute__((aligned(16))) uint32_t s_bm[IB][kThreads];   // the chunk's block minima
+    // every row's lines (thread t: row i = t, once per workgroup) and each
+    // chunk's degenerate flag
+    __shared__ LineRec s_r13[kThreads], s_r12[kThreads], s_c12[kJ], s_r23[kJ];
+    __shared__ double s_p0[kThreads][2], s_p1[kJ][2];
+    __shared__ int32_t s_degc[kThreads / IB];
+    __shared__ __attribute__((aligned(16))) uint16_t s_bm[IB][kThreads];   // the chunk's block minima (16-bit)
 
     const int t = threadIdx.x;
     uint32_t blk = blockIdx.x;   // each XCD a contiguous range of (scene, j block)s
@@ -1608,8 +1609,30 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
         c23.deg = col_line(f, kx, ky, c23.l0, c23.l1, c23.l2) ? 1.0 : 0.0;
         any_deg |= (cl13.deg != 0.0) || (c23.deg != 0.0);
     }
+    {   // row i = t's lines; a chunk (16 rows of one wave) is degenerate when
+        // any of its rows is
+        LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
+        double px = 0.0, py = 0.0;
+        if (t < N) {
+            double f[9];
+            px = args.pts[2 * (c0 + t)];
+            py = args.pts[2 * (c0 + t) + 1];
+            load_f(F13, f);
+            a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
+            load_f(F12, f);
+            b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
+        }
+        s_r13[t] = a;
+        s_r12[t] = b;
+        s_p0[t][0] = px;
+        s_p0[t][1] = py;
+        static_assert(kWave % IB == 0, "a wave's rows: whole chunks");
+        const uint64_t dm = __ballot((a.deg != 0.0) || (b.deg != 0.0));
+        if (t % kWave < kWave / IB)
+            s_degc[t / kWave * (kWave / IB) + t % kWave] = ((dm >> (IB * (t % kWave))) & ((1ull << IB) - 1)) != 0;
+    }
     // uniform: no j / k line of the workgroup is degenerate (the rows' lines
-    // are judged per chunk)
+    // are judged per chunk: s_degc)
     const bool deg_fixed = __syncthreads_or(any_deg) != 0;
     auto pair = [&](bool nd, const LineRec &col, const LineRec &row, double rx, double ry, double cx,
                     double cy) {
@@ -1650,36 +1673,15 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     // ---- the scene's i rows, IB at a time --------------------------------------
     for (int i0 = 0; i0 < N; i0 += IB) {
         const int ni = min(IB, N - i0);
-        const int cb = (i0 / IB) & 1;            // this chunk's row-line buffer
-        bool deg_rows = false;
-        static_assert(IB <= kWave, "the chunk's row lines: one thread of wave 0 each");
-        if (t < IB) {
-            LineRec a{0.0, 0.0, 0.0, 0.0}, b{0.0, 0.0, 0.0, 0.0};
-            double px = 0.0, py = 0.0;
-            if (t < ni) {
-                double f[9];
-                px = args.pts[2 * (c0 + i0 + t)];
-                py = args.pts[2 * (c0 + i0 + t) + 1];
-                load_f(F13, f);
-                a.deg = row_line(f, px, py, a.l0, a.l1, a.l2) ? 1.0 : 0.0;
-                load_f(F12, f);
-                b.deg = row_line(f, px, py, b.l0, b.l1, b.l2) ? 1.0 : 0.0;
-            }
-            deg_rows = (a.deg != 0.0) || (b.deg != 0.0);
-            s_r13[cb][t] = a;
-            s_r12[cb][t] = b;
-            s_p0[cb][t][0] = px;
-            s_p0[cb][t][1] = py;
-        }
-        // (the barrier also puts every wave past the previous chunk's reads of
-        // s12 / s12f: it must run whatever deg_fixed is -- no short circuit)
-        const bool deg_chunk = __syncthreads_or(deg_rows) != 0;
+        // (every wave past the previous chunk's reads of s12 / s12f)
+        __syncthreads();
+        const bool deg_chunk = s_degc[i0 / IB] != 0;
         const bool nd = !deg_fixed && !deg_chunk;
         bool near_c = near;
         for (int x = t; x < IB * kJ; x += kThreads) {
             const int r = x / kJ, jj = x % kJ;
             const bool v = r < ni && jj < nj;
-            const double e = v ? pair(nd, s_c12[jj], s_r12[cb][r], s_p0[cb][r][0], s_p0[cb][r][1],
+            const double e = v ? pair(nd, s_c12[jj], s_r12[i0 + r], s_p0[i0 + r][0], s_p0[i0 + r][1],
                                       s_p1[jj][0], s_p1[jj][1])
                                : 0.0;
             s12[r][jj] = e;
@@ -1691,7 +1693,7 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
         for (int ii = 0; ii < ni; ++ii) {
             const int i = i0 + ii;
             const double e13 =
-                kv ? pair(nd, cl13, s_r13[cb][ii], s_p0[cb][ii][0], s_p0[cb][ii][1], kx, ky) : 0.0;
+                kv ? pair(nd, cl13, s_r13[i], s_p0[i][0], s_p0[i][1], kx, ky) : 0.0;
             if (jb == 0 && kv) E13T[(int64_t)k * ld + i] = e13;
             // every residual of the wave's rows <= kApproxResidual (wave-uniform)
             const bool fast = chunk_near && __all(e13 <= kApproxResidual);
@@ -1760,15 +1762,15 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                     if (kv && B8) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
                 }
             }
-            // sp_bmin8_reduce_kernel's upper bound of the block minimum
-            s_bm[ii][t] = umin((hmin << 16) | 0xFFFFu, 0xFF800000u);
+            s_bm[ii][t] = (uint16_t)hmin;        // (its upper bound at the chunk's end)
         }
         // the chunk's 16 block minima of column k: one 64-byte run (rows past
         // the view never a candidate)
         if (kv) {
             uint32_t v[IB];
 #pragma unroll
-            for (int ii = 0; ii < IB; ++ii) v[ii] = ii < ni ? s_bm[ii][t] : 0xFFFFFFFFu;
+            for (int ii = 0; ii < IB; ++ii)      // sp_bmin8_reduce_kernel's upper bound of the block minimum
+                v[ii] = ii < ni ? umin(((uint32_t)s_bm[ii][t] << 16) | 0xFFFFu, 0xFF800000u) : 0xFFFFFFFFu;
 #pragma unroll
             for (int ii = 0; ii < IB; ii += 4)
                 *reinterpret_cast<uint4 *>(BM + i0 + ii) = make_uint4(v[ii], v[ii + 1], v[ii + 2], v[ii + 3]);
