@@ -537,7 +537,7 @@ def run_match(args, env, wl, kernel_options):
         raise SystemExit(3)
 
 
-FREE_LSAP_INPUT = "bmin8"      # the cube-free chain's default block source (--lsap-input auto)
+FREE_LSAP_INPUT = "blocks"     # the cube-free chain's default block source (--lsap-input auto)
 
 
 def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free", cpu_seconds=0.0,

@@ -1535,7 +1535,7 @@ struct MinimaArgs {
     int32_t j_blocks;
 };
 
-template <int IB>
+template <int IB, bool G8>   // G8: the 8-row minima too (else the block minima only)
 __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs args) {
     constexpr int kJ = 32;                     // j per workgroup: four 8-row groups
     static_assert(IB == 16, "the chunk's block minima leave as one 64-byte run per k");
@@ -1700,7 +1700,37 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
             // the four groups' keys (a group past the view -- all its e23
             // +inf -- is computed and ignored below)
             uint32_t key[kJ / 8];
-            if (fast) {
+            uint32_t hmin = 0xFFFFu;             // the block's smallest 16-bit key
+            if (!G8 && fast) {
+                // the block's minimum over its 32 j at once, the same float32
+                // sums and recheck as the groups' below
+                const float f13 = (float)e13;
+                float v[kJ];
+#pragma unroll
+                for (int r = 0; r < kJ; r += 4) {
+                    const f32x4 w = *reinterpret_cast<const f32x4 *>(&s12f[ii][r]);
+                    v[r] = w.x + f23[r];
+                    v[r + 1] = w.y + f23[r + 1];
+                    v[r + 2] = w.z + f23[r + 2];
+                    v[r + 3] = w.w + f23[r + 3];
+                }
+#pragma unroll
+                for (int w = kJ / 2; w >= 1; w /= 2)
+#pragma unroll
+                    for (int r = 0; r < w; ++r) v[r] = __builtin_fminf(v[r], v[r + w]);
+                uint32_t b = __float_as_uint((v[0] + f13) * kThirdF);
+                const bool ok = !kv || ((b & 0xFFFFu) - kApproxMargin < 0x10000u - 2 * kApproxMargin &&
+                                        b >= kApproxTiny);
+                if (!ok) {                               // exact: 32 fp64 sums, e23 from this thread's e23T row
+                    const double *e23r = E23T + (int64_t)k * ld + jw0;
+                    double sm = (double)INFINITY;
+#pragma unroll 4
+                    for (int jj = 0; jj < kJ; ++jj)
+                        sm = fmin(sm, (s12[ii][jj] + e13) + (jj < nj ? e23r[jj] : (double)INFINITY));   // :81
+                    b = __float_as_uint((float)third_q(sm));
+                }
+                hmin = (b | 0x80000000u) >> 16;
+            } else if (fast) {
                 const float f13 = (float)e13;
 #pragma unroll
                 for (int g = 0; g < kJ / 8; ++g) {
@@ -1753,13 +1783,14 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                     key[g] = kk;
                 }
             }
-            uint32_t hmin = 0xFFFFu;             // the block's smallest 16-bit key
+            if (G8 || !fast) {
 #pragma unroll
-            for (int g = 0; g < kJ / 8; ++g) {
-                if (8 * g < nj) {                // uniform
-                    const uint32_t h = key[g] >> 16;
-                    hmin = umin(hmin, h);
-                    if (kv && B8) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
+                for (int g = 0; g < kJ / 8; ++g) {
+                    if (8 * g < nj) {            // uniform
+                        const uint32_t h = key[g] >> 16;
+                        hmin = umin(hmin, h);
+                        if (G8 && kv) B8[((int64_t)i * g8 + 4 * jb + g) * P + k] = (uint16_t)h;
+                    }
                 }
             }
             s_bm[ii][t] = (uint16_t)hmin;        // (its upper bound at the chunk's end)
@@ -1896,8 +1927,12 @@ int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const
     a.j_blocks = (max_n + 31) / 32;
     const int64_t blocks = (int64_t)n_scenes * a.j_blocks;
     if ((st = grid_check(blocks))) return st;
-    triplet_minima_kernel<16><<<dim3((unsigned)blocks), dim3(kThreads), 0,
-                                reinterpret_cast<hipStream_t>(stream)>>>(a);
+    if (bmin8_dev)
+        triplet_minima_kernel<16, true><<<dim3((unsigned)blocks), dim3(kThreads), 0,
+                                          reinterpret_cast<hipStream_t>(stream)>>>(a);
+    else
+        triplet_minima_kernel<16, false><<<dim3((unsigned)blocks), dim3(kThreads), 0,
+                                           reinterpret_cast<hipStream_t>(stream)>>>(a);
     return mvm_check_launch("triplet_minima_kernel");
 }
 

@@ -543,7 +543,9 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         // (from the cube's 16-bit minima, bm holds upper bounds: a block may
         // hold a cost <= theta when its lower bound, the upper half, is <= thr)
         const bool groups8 = seg0 && a.bmin8;              // refine them to 8-column groups
-        const KT lowmask = groups8 ? (KT)0xFFFF0000u : ~(KT)0;
+        // 16-bit-derived keys (the 8-row minima, or ext's block upper bounds)
+        // compare by their lower bound, the upper half
+        const KT lowmask = groups8 || ext ? (KT)0xFFFF0000u : ~(KT)0;
         int ncand = 0;
 #pragma unroll
         for (int q = 0; q < kQ; ++q) {

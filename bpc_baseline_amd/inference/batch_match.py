@@ -164,9 +164,11 @@ def _device_chain(pts, cam_offs, cam_offs_host, F_dev, proj_dev, S, threshold, c
     c3 = plan.counts
     mark("cube plan")
     if cube_free:
-        # the assignment never reads a cube: the 8-row minima it reduces and
-        # the fp64 pair residuals it recomputes its entries from
-        minima = ops.triplet_minima(pts, cam_offs, F_dev, plan)
+        # the assignment never reads a cube: the 32-column block minima its
+        # candidate lists start from and the fp64 pair residuals it recomputes
+        # its entries from (no 8-row minima: the lists gather
+        # whole candidate blocks)
+        minima = ops.triplet_minima(pts, cam_offs, F_dev, plan, with_bmin8=False)
         mark("cube")
         lplan = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
         mark("lsap plan")

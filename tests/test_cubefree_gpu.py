@@ -117,6 +117,11 @@ def test_minima_nonfinite_chunks(cuda):
             o32 = plan.bm32_offs_host[s]
             want32 = _want_bm32(O.bmin8_keys(cs), N, M, Pn).reshape(-1)
             assert np.array_equal(got32[o32:o32 + want32.size], want32), (kw, s, "block minima")
+        # the block minima alone (no 8-row minima): the same bits
+        from bpc_baseline_amd import ops
+        t = lambda a: torch.from_numpy(a).to(cuda)
+        _, bm32_only = ops.triplet_minima(t(pts), t(co), t(F), plan, with_bmin8=False)
+        assert torch.equal(bm32_only[:plan.n_bm32], bm32[:plan.n_bm32]), kw
 
 
 def _assign_both(cuda, counts, seed, options=None, **kw):
