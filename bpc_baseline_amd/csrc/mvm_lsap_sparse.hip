@@ -114,6 +114,24 @@ __device__ __forceinline__ int sp_wave_min_i32(int x) {
                min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 
+__device__ __forceinline__ float sp_first_lane(float x) {
+    return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ double sp_first_lane(double x) {
+    const long long b = __double_as_longlong(x);
+    return __longlong_as_double(((long long)__builtin_amdgcn_readfirstlane((int)(b >> 32)) << 32) |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)b));
+}
+
+__device__ __forceinline__ uint32_t sp_wave_max_u32(uint32_t x) {
+    x = max(x, (uint32_t)sp_dpp_i32<0xB1>((int)x));
+    x = max(x, (uint32_t)sp_dpp_i32<0x4E>((int)x));
+    x = max(x, (uint32_t)sp_dpp_i32<0x141>((int)x));
+    x = max(x, (uint32_t)sp_dpp_i32<0x140>((int)x));
+    return max(max((uint32_t)__builtin_amdgcn_readlane((int)x, 0), (uint32_t)__builtin_amdgcn_readlane((int)x, 16)),
+               max((uint32_t)__builtin_amdgcn_readlane((int)x, 32), (uint32_t)__builtin_amdgcn_readlane((int)x, 48)));
+}
+
 __device__ __forceinline__ long long sp_wave_max_i64(long long x) {
     for (int o = 1; o < 64; o <<= 1) {
         const long long y = __shfl_xor(x, o);
@@ -530,13 +548,25 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
             // blocks l, l + 64, ...), so >= tb blocks hold a cost <= theta;
             // a search over one value per lane (32 steps of one compare), where
             // the tb-th smallest block minimum itself took 32 compares per step
-            KT lo = 0, hi = K::kMax;
-            while (lo < hi) {
-                const KT mid = lo + (hi - lo) / 2;
-                if (__popcll(__ballot(lm <= mid)) >= a.tb) hi = mid;
-                else lo = mid + 1;
+            if constexpr (ext) {
+                // ext keys are (h << 16) | 0xFFFF (or kMax): search h, 16 steps
+                uint32_t lo = 0, hi = 0xFFFFu;
+                const uint32_t lh = (uint32_t)(lm >> 16);
+                while (lo < hi) {
+                    const uint32_t mid = lo + (hi - lo) / 2;
+                    if (__popcll(__ballot(lh <= mid)) >= a.tb) hi = mid;
+                    else lo = mid + 1;
+                }
+                thr = (KT)((lo << 16) | 0xFFFFu);
+            } else {
+                KT lo = 0, hi = K::kMax;
+                while (lo < hi) {
+                    const KT mid = lo + (hi - lo) / 2;
+                    if (__popcll(__ballot(lm <= mid)) >= a.tb) hi = mid;
+                    else lo = mid + 1;
+                }
+                thr = lo;
             }
-            thr = lo;
             theta = K::val(thr);
         }
         // candidate blocks (uniform count): every block holding a cost <= theta
@@ -653,7 +683,8 @@ struct SpRec {
     int32_t a_ps;      // its path step
     int32_t f_any;     // some list entry of the wave is free
     int32_t tail_q;    // the slot at scan position n_rem - 1 (-1: none in this wave)
-    int32_t pad;
+    uint32_t f_key;    // first step: the latest-in-scan-order key among the wave's free
+                       // list entries at f ((L-1-c) << 16 | c; 0: none)
 };
 
 // dynamic LDS of sp_solve_kernel: bitmaps of lw words, row and step arrays of cap
@@ -682,7 +713,7 @@ __device__ __forceinline__ long long sp_block_max_i64(long long x, long long *s_
 }
 
 template <typename CT, int KS>
-__global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32_t n, int32_t lw) {
+__global__ __launch_bounds__(kSpNT) __attribute__((amdgpu_waves_per_eu(KS == 1 ? 4 : 1))) void sp_solve_kernel(LsapSparseArgs a, int32_t n, int32_t lw) {
     __shared__ SpRec s_rec[2][kSpNT / 64];
     __shared__ double s_redd[kSpNT / 64];
     __shared__ long long s_redl[kSpNT / 64];
@@ -788,9 +819,52 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
     auto mvd = [&](int j) { return (s_mvb[j >> 5] >> (j & 31)) & 1u; };
     auto rfree = [](double mp, CT c, double ui) { return ((mp + (double)c) - ui) - 0.0; };
 
+    // a step's row data: its list, theta, and the raw entries at the slots'
+    // columns (resid: the e13T / e23T values; else the cost).  The first step
+    // of search cur + 1 visits row cur + 1, so its loads are issued during
+    // search cur and stay in flight across its barriers (which wait for LDS
+    // only); a slot assigned at the end of search cur loads its own then
+    struct RowData {
+        int nl;                                               // (lane 0 of each wave: the row's
+        CT th;                                                //  values, broadcast where used)
+        int lc;
+        CT lv;
+        double x[KS], y[KS];                                  // resid: e13T, e23T; else x = the cost
+    };
+    auto load_row = [&](int i_any, int n_slots) {
+        const int i = __builtin_amdgcn_readfirstlane(i_any);   // uniform
+        RowData d;
+        // one lane loads them, so nothing converts them to scalars (a wait
+        // for the load) before the step that uses them
+        d.nl = lane == 0 ? ln[i] : 0;
+        d.th = lane == 0 ? theta[i] : (CT)0;
+        d.lc = 0;
+        d.lv = (CT)0;
+        if (t < kSpLCap) {
+            d.lc = lcol[(int64_t)i * kSpLCap + t];
+            d.lv = lval[(int64_t)i * kSpLCap + t];
+        }
+#pragma unroll
+        for (int m = 0; m < KS; ++m) {
+            const bool has = t + kSpNT * m < n_slots;
+            d.x[m] = d.y[m] = 0.0;
+            if (src.e12) {
+                if (has) {
+                    d.x[m] = src.e13t[i * src.ld + sic[m]];
+                    d.y[m] = src.e23t[i * src.ld + sjc[m]];
+                }
+            } else if (has) {
+                d.x[m] = (double)src.at(i, col[m]);
+            }
+        }
+        return d;
+    };
+    RowData pf = load_row(0, 0);                              // search 0's first step
+
     int par = 0;
     for (int cur = 0; cur < S; ++cur) {
         const int na = cur;                                   // slots 0 .. na-1 are assigned columns
+        RowData rd = pf;
 #pragma unroll
         for (int m = 0; m < KS; ++m) {
             spc[m] = INFINITY;
@@ -803,27 +877,23 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
         int sink = -1, sink_ps = -1;
         while (true) {
             // ---- one Dijkstra step: every load of the step in flight at once
+            // (the first step's were issued during the previous search)
+            if (k > 0) rd = load_row(i, na);
             const double ui = s_u[i];
-            const int nl = ln[i];
-            const CT th = theta[i];
+            const int nl = __builtin_amdgcn_readfirstlane(rd.nl);
+            const CT th = sp_first_lane(rd.th);
             CT cv[KS];
 #pragma unroll
             for (int m = 0; m < KS; ++m) {
                 const int q = t + kSpNT * m;
                 const bool live = q < na && !((rem >> m) & 1u);
                 if (src.e12)
-                    cv[m] = live ? (CT)cube_f32(se12[m], src.e13t[i * src.ld + sic[m]],
-                                                src.e23t[i * src.ld + sjc[m]])
-                                 : (CT)0;
+                    cv[m] = live ? (CT)cube_f32(se12[m], rd.x[m], rd.y[m]) : (CT)0;
                 else
-                    cv[m] = live ? src.at(i, col[m]) : (CT)0;
+                    cv[m] = live ? (CT)rd.x[m] : (CT)0;
             }
-            int lc = 0;
-            CT lv = (CT)0;
-            if (t < kSpLCap) {
-                lc = lcol[(int64_t)i * kSpLCap + t];
-                lv = lval[(int64_t)i * kSpLCap + t];
-            }
+            const int lc = rd.lc;
+            const CT lv = rd.lv;
             double ba = INFINITY;
             int bpos = 0x7FFFFFFF, bq = -1, bps = -1, tq = -1;
 #pragma unroll
@@ -863,11 +933,17 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                 const uint64_t fa = __ballot(fany);
                 const uint64_t tm = __ballot(tq >= 0);
                 const int wt = tm ? __builtin_amdgcn_readlane(tq, (int)__builtin_ctzll(tm)) : -1;
-                if (lane == 0) s_rec[par][wave] = SpRec{wa, wf, wpos, wq, wps, fa != 0, wt, 0};
+                // the first step's free ties, for the sink without the tie scan
+                // (no column is moved yet in a search's first step)
+                uint32_t wk = 0;
+                if (k == 0)
+                    wk = sp_wave_max_u32(fany && fr == wf ? ((uint32_t)(L - 1 - lc) << 16) | (uint32_t)lc : 0u);
+                if (lane == 0) s_rec[par][wave] = SpRec{wa, wf, wpos, wq, wps, fa != 0, wt, wk};
             }
             __syncthreads();
             double A = INFINITY, fk = INFINITY;
             int apos = 0x7FFFFFFF, aq = -1, aps = -1, f_any = 0, tail_q = -1;
+            uint32_t fkey = 0;
 #pragma unroll
             for (int w = 0; w < kSpNT / 64; ++w) {
                 const SpRec r = s_rec[par][w];
@@ -877,6 +953,8 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                     aq = r.a_q;
                     aps = r.a_ps;
                 }
+                if (r.f < fk) fkey = r.f_key;
+                else if (r.f == fk) fkey = max(fkey, r.f_key);
                 fk = fmin(fk, r.f);
                 f_any |= r.f_any;
                 tail_q = r.tail_q >= 0 ? r.tail_q : tail_q;
@@ -911,9 +989,24 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                 s_f[k] = fk;
                 s_rb[k] = rb;
             }
+            // the next search's first row, once this step's row data is used
+            // (issued earlier, a wait for this step's loads would cover them)
+            if (k == 0 && cur + 1 < S) pf = load_row(cur + 1, na);
             F = fmin(F, fk);
             lowest = fmin(A, F);
             if (!(lowest < INFINITY)) break;                  // infeasible
+            if (!(A < F) && k == 0 && fkey != 0 && fk == lowest && nl >= 0 && rb == rb && rb != lowest) {
+                // the search's first row holds the minimum in its list, and no
+                // entry off the list can tie: its latest tie is the sink
+                sink = (int)(fkey & 0xFFFFu);
+                sink_ps = 0;
+                if (t == 0) {
+                    s_m[k] = lowest;
+                    s_sl[k] = -1;
+                    s_ps[k] = 0;
+                }
+                break;
+            }
             if (!(A < F)) {
                 // a free column reaches the minimum: the one latest in scan
                 // order among every visited row's free ties is the sink
@@ -1037,6 +1130,14 @@ __global__ __launch_bounds__(kSpNT) void sp_solve_kernel(LsapSparseArgs a, int32
                     sic[m] = sp_div(sink, src.M, src.rM, jj);
                     sjc[m] = jj;
                     se12[m] = src.e12[sic[m] * src.ld + jj];
+                }
+                if (cur + 1 < S) {                            // its entry of the next search's first row
+                    if (src.e12) {
+                        pf.x[m] = src.e13t[(cur + 1) * src.ld + sic[m]];
+                        pf.y[m] = src.e23t[(cur + 1) * src.ld + sjc[m]];
+                    } else {
+                        pf.x[m] = (double)src.at(cur + 1, sink);
+                    }
                 }
             }
         }

@@ -14,8 +14,8 @@ otherwise; the generator is bpc_baseline_amd.synth.make_scenes):
               everywhere: many near-equal candidates per row)
   quant1/quant8  the default cube with every cost rounded down to a multiple
               of 1 / 8 px (blocks of exactly equal costs)
-The cube-free chain (triplet_minima -> linear_sum_assignment_resid) runs the
-first five, the cube form (the quantised cube and its 8-row minima ->
+The cube-free chain (triplet_minima -> linear_sum_assignment_resid; block
+minima only unless --bmin8) runs the first five, the cube form (the quantised cube and its 8-row minima ->
 linear_sum_assignment_batched) the last two.  Per case: the assignment's ms
 (HIP events, best and median of --reps), and the solver's counters per batch
 (ops.lsap_sparse_stats: dense free-minimum scans, dense tie scans, overflowed
@@ -41,6 +41,9 @@ ap.add_argument("--dets", type=int, default=256)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--cases", default="default,dup10,dup30,clutter,objects,quant1,quant8")
 ap.add_argument("--json", default=None, help="also write the table here")
+ap.add_argument("--bmin8", action="store_true",
+                help="cube-free cases with the 8-row minima (default: block minima only, "
+                     "what match_captures runs)")
 args = ap.parse_args()
 dev = torch.device("cuda", 0)
 S, n = args.scenes, args.dets
@@ -115,7 +118,7 @@ for case in args.cases.split(","):
         fn = lambda: ops.linear_sum_assignment_batched(cube, offs, lp, bmin8=(bm8, tp.bmin8_offs, tp.segs))
         costs_host = lambda s: cube[tp.cube_offs_host[s]:tp.cube_offs_host[s + 1]].cpu().numpy()
     else:
-        bm8 = ops.triplet_minima(P, C, F, tp)           # (8-row minima, block minima)
+        bm8 = ops.triplet_minima(P, C, F, tp, with_bmin8=args.bmin8)   # (8-row minima, block minima)
         lp = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
         fn = lambda: ops.linear_sum_assignment_resid(lp, tp, bm8)
 
