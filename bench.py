@@ -608,7 +608,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
             # --lsap-input blocks: no 8-row minima (the lists gather whole blocks)
             ch["bm8"] = torch.empty(max(tp.n_bmin8, 1) if lsap_input == "bmin8" else 0,
                                     dtype=torch.int16, device=dev)
-            ch["bm32"] = torch.empty(max(tp.n_bm32, 4), dtype=torch.int32, device=dev)
+            ch["bm32"] = torch.empty(max(tp.n_bm32, 8), dtype=torch.int16, device=dev)
         else:
             ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
             ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
@@ -725,7 +725,7 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                     keys_ok = np.array_equal(keys, want8.reshape(-1))
                 want32 = O.bm32_keys(want8, *n3).reshape(-1)
                 o32 = int(tp.bm32_offs_host[sl])
-                keys_ok &= np.array_equal(ch["bm32"][o32:o32 + want32.size].cpu().numpy().view(np.uint32),
+                keys_ok &= np.array_equal(ch["bm32"][o32:o32 + want32.size].cpu().numpy().view(np.uint16),
                                           want32)
                 co1 = batch.cam_offs[3 * s:3 * s + 4]
                 want_r = O.residuals(batch.pts[int(co1[0]):int(co1[3])], co1 - co1[0],
@@ -781,8 +781,8 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
         n_bm32 = sum(ch["tplan"].n_bm32 for ch in chunks)
         n8w = n_bmin8 if lsap_input == "bmin8" else 0
         first_bytes = (16.0 * counts.sum() + 3 * 72.0 * len(N) + 2.0 * float(n8w)
-                       + 4.0 * float(n_bm32) + 8.0 * float((N * M + P * N + P * M).sum()))
-        lsap_bytes = 4.0 * float(n_bm32)
+                       + 2.0 * float(n_bm32) + 8.0 * float((N * M + P * N + P * M).sum()))
+        lsap_bytes = 2.0 * float(n_bm32)
         first_kernel = "triplet_minima_kernel"
     else:
         first_bytes = cb

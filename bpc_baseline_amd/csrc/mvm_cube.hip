@@ -1526,7 +1526,7 @@ struct MinimaArgs {
     const double *F;            // [S*3, 9]: F12, F13, F23
     uint16_t *bmin8;
     const int64_t *bmin8_offs;
-    uint32_t *bm32;
+    uint16_t *bm32;                 // 16-bit keys
     const int64_t *bm32_offs;
     double *resid;
     int64_t stride;             // doubles per scene
@@ -1575,7 +1575,7 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
     uint16_t *B8 = args.bmin8 ? args.bmin8 + args.bmin8_offs[s] : nullptr;   // optional
     const int npad = (N + 15) & ~15;
     const int nbk = ((M + 31) / 32) * npad;
-    uint32_t *BM = args.bm32 + args.bm32_offs[s] + (int64_t)k * nbk + (int64_t)jb * npad;
+    uint16_t *BM = args.bm32 + args.bm32_offs[s] + (int64_t)k * nbk + (int64_t)jb * npad;
 
     // ---- once per workgroup: the block's j lines, this thread's k lines -----
     bool any_deg = false;
@@ -1793,18 +1793,19 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
                     }
                 }
             }
-            s_bm[ii][t] = (uint16_t)hmin;        // (its upper bound at the chunk's end)
+            s_bm[ii][t] = (uint16_t)hmin;
         }
-        // the chunk's 16 block minima of column k: one 64-byte run (rows past
-        // the view never a candidate)
+        // the chunk's 16 block minima of column k: one 32-byte run of 16-bit
+        // keys (rows past the view 0xFFFF, never a candidate)
         if (kv) {
-            uint32_t v[IB];
+            uint32_t v[IB / 2];
 #pragma unroll
-            for (int ii = 0; ii < IB; ++ii)      // sp_bmin8_reduce_kernel's upper bound of the block minimum
-                v[ii] = ii < ni ? umin(((uint32_t)s_bm[ii][t] << 16) | 0xFFFFu, 0xFF800000u) : 0xFFFFFFFFu;
+            for (int ii = 0; ii < IB; ii += 2)
+                v[ii / 2] = (ii < ni ? (uint32_t)s_bm[ii][t] : 0xFFFFu) |
+                            ((ii + 1 < ni ? (uint32_t)s_bm[ii + 1][t] : 0xFFFFu) << 16);
 #pragma unroll
-            for (int ii = 0; ii < IB; ii += 4)
-                *reinterpret_cast<uint4 *>(BM + i0 + ii) = make_uint4(v[ii], v[ii + 1], v[ii + 2], v[ii + 3]);
+            for (int w = 0; w < IB / 2; w += 4)
+                *reinterpret_cast<uint4 *>(BM + i0 + 2 * w) = make_uint4(v[w], v[w + 1], v[w + 2], v[w + 3]);
         }
     }
 }
@@ -1890,7 +1891,7 @@ int mvm_triplet_cost_argmin_ex(const double *pts_dev, const int64_t *cam_offs_de
 
 int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                        int32_t n_scenes, int32_t max_n, uint16_t *bmin8_dev,
-                       const int64_t *bmin8_offs_dev, uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
+                       const int64_t *bmin8_offs_dev, uint16_t *bm32_dev, const int64_t *bm32_offs_dev,
                        double *resid_dev, size_t resid_bytes, const mvm_options *opts,
                        mvm_stream_t stream) {
     mvm_clear_error();

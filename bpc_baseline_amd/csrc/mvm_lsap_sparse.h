@@ -52,7 +52,7 @@ struct LsapSparseArgs {
     // pass, no block minima in the workspace): row s of problem p at bm32 +
     // bm32_offs[p] + s * ceil(seg/32) * roundup(L/seg, 16), block (jt, g) at
     // jt * roundup(L/seg, 16) + g
-    const uint32_t *bm32 = nullptr;
+    const uint16_t *bm32 = nullptr;                           // 16-bit keys
     const int64_t *bm32_offs = nullptr;
 };
 

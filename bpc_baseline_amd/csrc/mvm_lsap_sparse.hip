@@ -496,8 +496,8 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     // the blocks sit in mvm_triplet_minima's order, part-major -- b at
     // jt * npad + g of a row of bps * npad keys (segments padded to a multiple
     // of 16 with kMax) -- and lane l holds the 32 keys at 32 l .. 32 l + 31
-    // (one part, or two, of 32 consecutive segments: the same spread, eight
-    // 16-byte loads)
+    // (one part, or two, of 32 consecutive segments: the same spread, four
+    // 16-byte loads of 16-bit keys)
     const int bps = (seg + kSpBlock - 1) / kSpBlock, nseg = L / seg;
     const int nb = nseg * bps;
     const int npad = ext ? (nseg + 15) & ~15 : nseg;
@@ -512,29 +512,37 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         const int jt = sp_div(32 * lane + q, npad, rnpad, g);
         return g * bps + jt;
     };
-    const KT *bm = ext ? reinterpret_cast<const KT *>(a.bm32 + a.bm32_offs[p])
-                       : reinterpret_cast<const KT *>(ws + y.bm);
+    const KT *bm = reinterpret_cast<const KT *>(ws + y.bm);
+    const uint16_t *bm16 = ext ? a.bm32 + a.bm32_offs[p] : nullptr;   // ext: 16-bit keys
     int bad = 0;                                           // ext: a NaN entry (key 0) in these rows
     for (int s = grp * (kSpNT / 64) + wave; s < S; s += kSpRowGroups * (kSpNT / 64)) {
         KT k[kQ];
         // the row base wave-uniform (a scalar base + 32-bit lane offsets)
-        const KT *row = bm + (int64_t)__builtin_amdgcn_readfirstlane(s) * rowk;
+        const int64_t s_u = __builtin_amdgcn_readfirstlane(s);
         if constexpr (!ext) {
+            const KT *row = bm + s_u * rowk;
 #pragma unroll
             for (int q = 0; q < kQ; ++q) {
                 const int idx = lane + 64 * q;
                 k[q] = idx < nb ? row[idx] : K::kMax;
             }
         } else {
-            static_assert(kQ == 32 && sizeof(KT) == 4, "ext: 32 keys of 4 bytes per lane");
-            const uint4 *r4 = reinterpret_cast<const uint4 *>(row) + 8 * lane;
+            // 16-bit keys h: the block's upper bound (h << 16) | 0xFFFF, +inf's
+            // key for h = 0xFF80 (every entry +inf), 0xFFFF padding -> kMax
+            static_assert(kQ == 32 && sizeof(KT) == 4, "ext: 32 keys per lane");
+            const uint4 *r4 = reinterpret_cast<const uint4 *>(bm16 + s_u * rowk) + 4 * lane;
+            auto up = [](uint32_t h) -> KT {
+                return h == 0xFFFFu ? K::kMax : h >= 0xFF80u ? (KT)0xFF800000u : (KT)((h << 16) | 0xFFFFu);
+            };
 #pragma unroll
-            for (int v = 0; v < 8; ++v) {                  // rowk is a multiple of 16
-                const uint4 w = 32 * lane + 4 * v < rowk ? r4[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
-                k[4 * v] = w.x;
-                k[4 * v + 1] = w.y;
-                k[4 * v + 2] = w.z;
-                k[4 * v + 3] = w.w;
+            for (int v = 0; v < 4; ++v) {                  // rowk is a multiple of 16
+                const uint4 w = 32 * lane + 8 * v < rowk ? r4[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
+                const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    k[8 * v + 2 * e] = up(d[e] & 0xFFFFu);
+                    k[8 * v + 2 * e + 1] = up(d[e] >> 16);
+                }
             }
         }
         KT lm = k[0];                                      // this lane's smallest block key
@@ -1281,7 +1289,7 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
                          int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                          int64_t long_min, int64_t long_max, int64_t short_max,
                          const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
-                         const uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
+                         const uint16_t *bm32_dev, const int64_t *bm32_offs_dev,
                          const int64_t *segs_dev, const double *resid_dev, int32_t max_n,
                          const mvm_options *opts, mvm_stream_t stream) {
     mvm_clear_error();

@@ -282,7 +282,7 @@ def triplet_minima_out(pts: Tensor, cam_offs: Tensor, F: Tensor, n_scenes: int, 
     every scene's fp64 pair residuals, no cube (mvm_triplet_minima, ABI 7)."""
     _check_inputs(pts, cam_offs, F, n_scenes * 3, n_scenes * 3)
     for t, n, dt in ((bmin8, "bmin8", torch.int16), (bmin8_offs, "bmin8_offs", torch.int64),
-                     (bm32, "bm32", torch.int32), (bm32_offs, "bm32_offs", torch.int64),
+                     (bm32, "bm32", torch.int16), (bm32_offs, "bm32_offs", torch.int64),
                      (resid, "resid", torch.uint8)):
         _require(t, n, dt, pts.device)
     st = _native.load().mvm_triplet_minima(_p(pts), _p(cam_offs), _p(F), n_scenes, max_n, _p(bmin8),
@@ -312,7 +312,7 @@ def lsap_solve_resid_out(dims: Tensor, ws_offs: Tensor, out_offs: Tensor, worksp
                      (out_offs, "out_offs", torch.int64), (workspace, "workspace", torch.uint8),
                      (row_ind, "row_ind", torch.int64), (col_ind, "col_ind", torch.int64),
                      (status, "status", torch.int32), (bmin8, "bmin8", torch.int16),
-                     (bmin8_offs, "bmin8_offs", torch.int64), (bm32, "bm32", torch.int32),
+                     (bmin8_offs, "bmin8_offs", torch.int64), (bm32, "bm32", torch.int16),
                      (bm32_offs, "bm32_offs", torch.int64), (segs, "segs", torch.int64),
                      (resid, "resid", torch.uint8)):
         _require(t, n, dt, dev)
@@ -612,7 +612,7 @@ class TripletPlan:
         self.bmin8_offs_host = bm8
         self.n_bmin8 = int(bm8[-1])
         # the cube-free path's 32-column block minima (mvm_triplet_minima): per
-        # scene P rows of ceil(M/32) * roundup(N, 16) uint32
+        # scene P rows of ceil(M/32) * roundup(N, 16) 16-bit keys (32-byte runs)
         b32 = np.zeros(n_scenes + 1, np.int64)
         np.cumsum(counts[:, 2] * ((counts[:, 1] + 31) // 32) * ((counts[:, 0] + 15) // 16 * 16), out=b32[1:])
         self.bm32_offs_host = b32
@@ -655,7 +655,7 @@ def triplet_minima(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, 
     """Cube-free input of the assignment (mvm_triplet_minima, ABI 7): the
     cube's 8-row minima (int16 [plan.n_bmin8], the same bits
     ``triplet_cost_argmin(..., bmin8=)`` writes), the assignment's 32-column
-    block minima (int32 [plan.n_bm32]) and every scene's fp64 pair residuals,
+    block minima (16-bit keys, int16 [plan.n_bm32]) and every scene's fp64 pair residuals,
     written into ``plan.workspace`` (which the default cube kernels do not
     use; a later cube launch on the plan with the workspace kernel would
     overwrite them).  -> (bmin8, bm32).  Views of at most 256 detections.
@@ -666,7 +666,7 @@ def triplet_minima(pts: Tensor, cam_offs: Tensor, F: Tensor, plan: TripletPlan, 
     elif bmin8 is None:
         bmin8 = torch.empty(max(plan.n_bmin8, 1), dtype=torch.int16, device=pts.device)
     if bm32 is None:
-        bm32 = torch.empty(max(plan.n_bm32, 4), dtype=torch.int32, device=pts.device)
+        bm32 = torch.empty(max(plan.n_bm32, 8), dtype=torch.int16, device=pts.device)
     torch.ops.mvmatch.triplet_minima_out(pts, cam_offs, F, plan.n_scenes, plan.max_n, bmin8,
                                          plan.bmin8_offs, bm32, plan.bm32_offs, plan.workspace,
                                          _opts_list(options))

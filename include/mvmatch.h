@@ -272,15 +272,16 @@ int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs
  * flattened (N*M, P) cube that never reads the cube itself
  * (mvm_lsap_solve_resid, mvm_select_triangulate_resid), write only what
  * those need:
- *   bmin8_dev  the same 16-bit 8-row minima mvm_triplet_cost_argmin_bmin8
- *              writes (bit for bit, same layout and offsets);
- *   bm32_dev   the candidate-list kernels' 32-column block minima, as upper
- *              bounds: for short-side column k of scene s, nb = ceil(M/32) *
- *              npad uint32 at bm32_dev + bm32_offs_dev[s] + k * nb (npad =
- *              roundup(N, 16)), block (jt, i) at jt * npad + i holding
- *              min((h << 16) | 0xFFFF, 0xFF800000) for h the smallest 8-row
- *              key of columns i * M + 32 jt .. + 31, rows i >= N 0xFFFFFFFF;
- *              offsets multiples of 16 (16-byte aligned runs), bm32_dev
+ *   bmin8_dev  optional (NULL: not written): the same 16-bit 8-row minima
+ *              mvm_triplet_cost_argmin_bmin8 writes (bit for bit, same layout
+ *              and offsets);
+ *   bm32_dev   the candidate-list kernels' 32-column block minima as 16-bit
+ *              keys: for short-side column k of scene s, nb = ceil(M/32) *
+ *              npad keys at bm32_dev + bm32_offs_dev[s] + k * nb (npad =
+ *              roundup(N, 16)), block (jt, i) at jt * npad + i holding h, the
+ *              smallest 8-row key (upper half of the order-preserving float32
+ *              key, NaN 0) of columns i * M + 32 jt .. + 31; rows i >= N
+ *              0xFFFF; offsets multiples of 16 (32-byte runs), bm32_dev
  *              16-byte aligned;
  *   resid_dev  every scene's float64 pair residuals, from which the
  *              assignment recomputes the entries it reads as
@@ -292,12 +293,15 @@ int mvm_triplet_cost_argmin_bmin8(const double *pts_dev, const int64_t *cam_offs
  *              resid_bytes >= mvm_triplet_workspace_bytes(n_scenes, max_n)
  *              (16-byte aligned).
  * Views of at most 256 detections.  Replaces the cube's 4 B per triple of HBM
- * writes with ~0.5 B per 8 triples (epipolar_matching.py:83-98 feeding
- * :100-116).
+ * writes with 2 B per 32 triples (+ 2 B per 8 with bmin8_dev)
+ * (epipolar_matching.py:83-98 feeding :100-116).  The group and block
+ * minima are taken in float32 and every one within 8 units of a 16-bit carry
+ * is recomputed exactly in fp64, so the keys are those of the cube's own
+ * values bit for bit.
  */
 int mvm_triplet_minima(const double *pts_dev, const int64_t *cam_offs_dev, const double *F_dev,
                        int32_t n_scenes, int32_t max_n, uint16_t *bmin8_dev,
-                       const int64_t *bmin8_offs_dev, uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
+                       const int64_t *bmin8_offs_dev, uint16_t *bm32_dev, const int64_t *bm32_offs_dev,
                        double *resid_dev, size_t resid_bytes, const mvm_options *opts,
                        mvm_stream_t stream);
 
@@ -377,12 +381,14 @@ int mvm_lsap_solve_ex3(const void *cost_dev, int32_t cost_dtype, const int64_t *
 /*
  * Cube-free assignment (ABI 7): mvm_lsap_solve_ex3 for the flattened (N*M, P)
  * cubes of a mvm_triplet_minima batch, without the cubes.  Problem p is
- * scene p: dims (N*M, P), segs_dev[p] = M, its 8-row minima at bmin8_dev +
- * bmin8_offs_dev[p] and its pair residuals at resid_dev (max_n as given to
- * mvm_triplet_minima); the kernels recompute every entry they read with the
- * cube's arithmetic, so the result is that of mvm_lsap_solve_ex3 on the cubes
- * (and scipy's).  The candidate lists start from bm32_dev (mvm_triplet_minima's
- * block minima, no reduction pass).  There is no cost for the dense classes to read, so every
+ * scene p: dims (N*M, P), segs_dev[p] = M, its pair residuals at resid_dev
+ * (max_n as given to mvm_triplet_minima); the kernels recompute every entry
+ * they read with the cube's arithmetic, so the result is that of
+ * mvm_lsap_solve_ex3 on the cubes (and scipy's).  The candidate lists start
+ * from bm32_dev (mvm_triplet_minima's 16-bit block minima, no reduction pass)
+ * and, when bmin8_dev is not NULL, refine each candidate block to its 8-column
+ * groups by the 8-row minima at bmin8_dev + bmin8_offs_dev[p] (without them
+ * they gather whole blocks).  There is no cost for the dense classes to read, so every
  * non-empty problem must be of the candidate-list class (long sides >=
  * mvm_options.lsap_sparse_min_cols (default 4096) and > lsap_wave_max_cols
  * (1024), <= 65536; short sides <= 1024): the host bounds are checked
@@ -411,7 +417,7 @@ int mvm_lsap_solve_resid(const int64_t *dims_dev, int32_t n_problems, const int6
                          int64_t *row_ind_dev, int64_t *col_ind_dev, int32_t *status_dev,
                          int64_t long_min, int64_t long_max, int64_t short_max,
                          const uint16_t *bmin8_dev, const int64_t *bmin8_offs_dev,
-                         const uint32_t *bm32_dev, const int64_t *bm32_offs_dev,
+                         const uint16_t *bm32_dev, const int64_t *bm32_offs_dev,
                          const int64_t *segs_dev, const double *resid_dev, int32_t max_n,
                          const mvm_options *opts, mvm_stream_t stream);
 

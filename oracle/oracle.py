@@ -154,16 +154,14 @@ def bmin8_keys(cube: np.ndarray) -> np.ndarray:
 def bm32_keys(keys: np.ndarray, N: int, M: int, P: int) -> np.ndarray:
     """The 32-column block minima mvm_triplet_minima writes (include/mvmatch.h),
     from a scene's 8-row minima (bmin8_keys: uint16 [N, ceil(M/8), P]): per
-    (k, block jt of 32 j, i) the upper bound ((h << 16) | 0xFFFF, capped at
-    +inf's key) of the block's smallest 16-bit key h; rows i >= N 0xFFFFFFFF
-    -> uint32 [P, ceil(M/32), roundup(N, 16)]."""
+    (k, block jt of 32 j, i) the block's smallest 16-bit key; rows i >= N
+    0xFFFF -> uint16 [P, ceil(M/32), roundup(N, 16)]."""
     g8, bps, npad = (M + 7) // 8, (M + 31) // 32, (N + 15) // 16 * 16
-    pad = np.full((N, bps * 4, P), 0xFFFF, np.uint32)
+    pad = np.full((N, bps * 4, P), 0xFFFF, np.uint16)
     pad[:, :g8] = keys
     h = pad.reshape(N, bps, 4, P).min(axis=2)                         # [N, bps, P]
-    up = np.minimum((h << np.uint32(16)) | np.uint32(0xFFFF), np.uint32(0xFF800000))
-    out = np.full((P, bps, npad), 0xFFFFFFFF, np.uint32)
-    out[:, :, :N] = up.transpose(2, 1, 0)
+    out = np.full((P, bps, npad), 0xFFFF, np.uint16)
+    out[:, :, :N] = h.transpose(2, 1, 0)
     return out
 
 

@@ -275,5 +275,7 @@ def test_triplet_minima_validation(lib):
     assert lib.mvm_triplet_minima(None, None, None, 0, 0, None, None, None, None, None, 0, None, None) == 0
     assert lib.mvm_triplet_minima(FAKE, FAKE, FAKE, 10, 200, FAKE, FAKE, ctypes.c_void_p(0x1004), FAKE,
                                   FAKE, need, None, None) == 1      # misaligned block minima
+    assert lib.mvm_triplet_minima(FAKE, FAKE, FAKE, 10, 200, FAKE, None, FAKE, FAKE,
+                                  FAKE, need, None, None) == 1      # 8-row minima without offsets
     assert lib.mvm_select_triangulate_resid(None, 10, FAKE, FAKE, FAKE, FAKE, FAKE, FAKE, 3, 30.0,
                                             FAKE, FAKE, FAKE, FAKE, None) == 1

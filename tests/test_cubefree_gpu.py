@@ -44,7 +44,7 @@ def _minima(cuda, counts, seed, options=None, **kw):
     t = lambda a: torch.from_numpy(a).to(cuda)
     P, C, FF = t(pts), t(co), t(F)
     bm8 = torch.full((max(plan.n_bmin8, 1),), -1, dtype=torch.int16, device=cuda)
-    bm32 = torch.full((max(plan.n_bm32, 4),), 0x5A5A5A5A, dtype=torch.int32, device=cuda)
+    bm32 = torch.full((max(plan.n_bm32, 8),), 0x5A5A, dtype=torch.int16, device=cuda)
     plan.workspace.fill_(0xFF)                       # NaN everywhere the kernel does not write
     minima = ops.triplet_minima(P, C, FF, plan, bmin8=bm8, bm32=bm32, options=options)
     return plan, minima, (pts, F, co), (P, C, FF)
@@ -73,7 +73,7 @@ def test_minima_equal_cube_kernel_and_oracle(cuda, batch):
     counts = MINIMA_BATCHES[batch]
     plan, (bm8, bm32), (pts, F, co), (P, C, FF) = _minima(cuda, counts, 5)
     got = bm8.cpu().numpy().view(np.uint16)
-    got32 = bm32.cpu().numpy().view(np.uint32)
+    got32 = bm32.cpu().numpy().view(np.uint16)
     # the cube kernel's own minima on the same batch
     ref8 = torch.full_like(bm8, -1)
     cube, _, _ = ops.triplet_cost_argmin(P, C, FF, plan, bmin8=ref8)
@@ -108,7 +108,7 @@ def test_minima_nonfinite_chunks(cuda):
                {"nan_scene": 2, "nan_view": 2}, {"degenerate_scene": 1}):
         plan, (bm8, bm32), (pts, F, co), _ = _minima(cuda, counts, 9, **kw)
         got = bm8.cpu().numpy().view(np.uint16)
-        got32 = bm32.cpu().numpy().view(np.uint32)
+        got32 = bm32.cpu().numpy().view(np.uint16)
         oc = O.cube(pts, co, F, len(counts))[0]
         for s, (N, M, Pn) in enumerate(counts):
             o, n8 = plan.bmin8_offs_host[s], N * ((M + 7) // 8) * Pn
