@@ -70,7 +70,7 @@ pmc)
   W=$1; shift
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 300 rocprofv3 --pmc $C --output-format csv -d "$O/pmc_${C}_$W" -o run -- \
-      python bench.py --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 "$@" \
+      python bench.py --workload "$W" --steps 1 --warmup 0 --cpu-seconds 0 --c2match off "$@" \
       > "$O/pmc_${C}_$W.log" 2>&1 || fail "pmc $C $W" "$O/pmc_${C}_$W.log"
   done
   echo "pmc $W ok" ;;
@@ -92,6 +92,7 @@ final)
     bash "$0" trace "$W" || exit 1
     bash "$0" pmc "$W" || exit 1
   done
+  bash "$0" trace c2match || echo "c2match trace: see $O/trace_c2match.err"
   echo final ok ;;
 slots)
   OPT=${1:+--options $1}
