@@ -1689,8 +1689,57 @@ __global__ __launch_bounds__(kThreads, 4) void triplet_minima_kernel(MinimaArgs 
             near_c &= e <= kApproxResidual;
             if (v) E12[(int64_t)(i0 + r) * ld + jw0 + jj] = e;
         }
+        // block minima of a whole chunk: this thread's 16 e13 first (their
+        // fp64 lines and e13T stores together, float32 kept in registers),
+        // then the 16 rows unrolled so the LDS reads of one row overlap the
+        // sums of another
+        const bool whole = !G8 && ni == IB;      // uniform
+        float f13r[IB];
+        if (whole) {
+#pragma unroll
+            for (int ii = 0; ii < IB; ii += 2) {
+                const double a0 = kv ? pair(nd, cl13, s_r13[i0 + ii], s_p0[i0 + ii][0], s_p0[i0 + ii][1], kx, ky) : 0.0;
+                const double a1 =
+                    kv ? pair(nd, cl13, s_r13[i0 + ii + 1], s_p0[i0 + ii + 1][0], s_p0[i0 + ii + 1][1], kx, ky) : 0.0;
+                near_c &= a0 <= kApproxResidual && a1 <= kApproxResidual;
+                f13r[ii] = (float)a0;
+                f13r[ii + 1] = (float)a1;
+                if (jb == 0 && kv) *reinterpret_cast<f64x2 *>(E13T + (int64_t)k * ld + i0 + ii) = f64x2{a0, a1};
+            }
+        }
         const bool chunk_near = __syncthreads_and(near_c) != 0;
-        for (int ii = 0; ii < ni; ++ii) {
+        if (whole && chunk_near) {
+#pragma unroll
+            for (int ii = 0; ii < IB; ++ii) {
+                float v[kJ];
+#pragma unroll
+                for (int r = 0; r < kJ; r += 4) {
+                    const f32x4 w = *reinterpret_cast<const f32x4 *>(&s12f[ii][r]);
+                    v[r] = w.x + f23[r];
+                    v[r + 1] = w.y + f23[r + 1];
+                    v[r + 2] = w.z + f23[r + 2];
+                    v[r + 3] = w.w + f23[r + 3];
+                }
+#pragma unroll
+                for (int w = kJ / 2; w >= 1; w /= 2)
+#pragma unroll
+                    for (int r = 0; r < w; ++r) v[r] = __builtin_fminf(v[r], v[r + w]);
+                uint32_t b = __float_as_uint((v[0] + f13r[ii]) * kThirdF);
+                const bool ok = !kv || ((b & 0xFFFFu) - kApproxMargin < 0x10000u - 2 * kApproxMargin &&
+                                        b >= kApproxTiny);
+                if (!ok) {                               // exact: 32 fp64 sums (see the row loop below)
+                    const double e13 = pair(nd, cl13, s_r13[i0 + ii], s_p0[i0 + ii][0], s_p0[i0 + ii][1], kx, ky);
+                    const double *e23r = E23T + (int64_t)k * ld + jw0;
+                    double sm = (double)INFINITY;
+#pragma unroll 4
+                    for (int jj = 0; jj < kJ; ++jj)
+                        sm = fmin(sm, (s12[ii][jj] + e13) + (jj < nj ? e23r[jj] : (double)INFINITY));   // :81
+                    b = __float_as_uint((float)third_q(sm));
+                }
+                s_bm[ii][t] = (uint16_t)((b | 0x80000000u) >> 16);
+            }
+        }
+        for (int ii = 0; ii < ni && !(whole && chunk_near); ++ii) {
             const int i = i0 + ii;
             const double e13 =
                 kv ? pair(nd, cl13, s_r13[i], s_p0[i][0], s_p0[i][1], kx, ky) : 0.0;
