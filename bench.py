@@ -1444,6 +1444,11 @@ def main():
         if args.graph == "steps2":
             alt = torch.cuda.Stream(dev)
             q0, q1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            # the stream held by a spin kernel while the host enqueues the
+            # probes (eager launches and stream switches would otherwise leave
+            # gaps the steps2 graph does not have)
+            if hasattr(torch.cuda, "_sleep"):
+                torch.cuda._sleep(20_000_000)
             q0.record(stream)
             alt.wait_stream(stream)
             for rep in range(5):
