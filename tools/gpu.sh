@@ -192,6 +192,35 @@ cfab)
     python tools/summarise_sq.py "$O/sq_cf/run_counter_collection.csv" $K 16777216000 --what "c2match free $K" \
       --out "$O/sq_cf_$K.json" | grep -E "valu_|wait_over|SQ_" | tr -d '\n'; echo
   done ;;
+cubepin)
+  # the mid-size cube, kept build against the store-only
+  # diagnostic (tools/diag/cube_storeonly.patch) on the same buffers, then
+  # SQ and L2->DRAM write-path counters per build at the sizes named
+  K=bpc_baseline_amd/lib/ab/kept.so; SO=bpc_baseline_amd/lib/ab/cube_storeonly.so
+  for D in ${CP_SIZES:-100 130 150 256}; do
+    SC=$(python -c "print(max(1,int(8e9/(4*$D**3))))")
+    timeout -k 10 300 python -u tools/ab_same_buffers.py --libs "$K,$SO" --workload cube --dets "$D" \
+      --scenes "$SC" --buffers 3 --rounds 2 --no-check > "$O/pin_ab_$D.log" 2>&1 || fail "pin ab $D" "$O/pin_ab_$D.log"
+    echo "$D^3 ($SC scenes): $(tail -1 "$O/pin_ab_$D.log")"
+  done
+  for D in ${CP_PMC_SIZES:-100 130}; do
+    SC=$(python -c "print(max(1,int(8e9/(4*$D**3))))")
+    for L in kept cube_storeonly; do
+      i=0
+      for PM in "SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT" \
+                "TCC_EA0_WRREQ_STALL_sum TCC_EA0_WRREQ_DRAM_CREDIT_STALL_sum TCC_TOO_MANY_EA_WRREQS_STALL_sum TCC_EA0_WRREQ_LEVEL_sum" \
+                "SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE"; do
+        i=$((i+1))
+        timeout -s KILL 150 rocprofv3 --pmc $PM --output-format csv -d "$O/pin_pmc_${L}_${D}_$i" -o run -- \
+          python tools/ab_same_buffers.py --libs "bpc_baseline_amd/lib/ab/$L.so" --workload cube --dets "$D" \
+          --scenes "$SC" --buffers 1 --rounds 1 --no-check > "$O/pin_pmc_${L}_${D}_$i.log" 2>&1 \
+          || fail "pin pmc $L $D $i" "$O/pin_pmc_${L}_${D}_$i.log"
+        python tools/summarise_sq.py "$O/pin_pmc_${L}_${D}_$i/run_counter_collection.csv" triplet_ \
+          $((SC * D * D * D)) --what "$L $D^3 pass $i" --out "$O/pin_pmc_${L}_${D}_$i.json" > /dev/null
+      done
+      echo "pmc $L $D^3 ok"
+    done
+  done ;;
 ab)
   for rnd in $(seq 1 "${AB_ROUNDS:-3}"); do
     for lib in $AB_LIBS; do
