@@ -528,7 +528,8 @@ def run_match(args, env, wl, kernel_options):
     """``--workload c2match``: match_line() printed as the run's JSON line."""
     line, ok = match_line(args, env, wl, kernel_options, steps=args.steps, warmup=args.warmup,
                           cube_mode=args.cube, cpu_seconds=args.cpu_seconds,
-                          n_chunks_req=args.match_chunks, lsap_input=args.lsap_input)
+                          n_chunks_req=args.match_chunks, lsap_input=args.lsap_input,
+                          pipeline=args.match_pipeline == "on")
     if line is None:
         return
     print(json.dumps(line), flush=True)
@@ -541,7 +542,7 @@ FREE_LSAP_INPUT = "blocks"     # the cube-free chain's default block source (--l
 
 
 def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free", cpu_seconds=0.0,
-               n_chunks_req=1, lsap_input="auto"):
+               n_chunks_req=1, lsap_input="auto", pipeline=False):
     """What ``match_objects`` returns, at C2 scale (the ``c2match`` workload).
 
     A step is every scene of this rank through the device chain of
@@ -584,45 +585,54 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
     # assignment overlaps the HBM-bound cube of the next chunk (the cube of a
     # chunk waits for the previous step's use of its buffers).  --match-chunks 1
     # is the serial chain.
+    # pipeline: consecutive steps overlap -- step t's assignment + select on the
+    # second stream while step t + 1's minima run on the launch stream -- over
+    # two buffer sets (a step waits only for step t - 2's use of its set), as a
+    # service matching a stream of capture batches would run them
     n_chunks = max(1, min(n_chunks_req, n_local))
     bounds = np.linspace(0, n_local, n_chunks + 1).astype(np.int64)
     stream = torch.cuda.current_stream(dev)
-    side = torch.cuda.Stream(dev) if n_chunks > 1 else stream
-    chunks = []
-    for a, b in zip(bounds[:-1], bounds[1:]):
-        a, b = int(a), int(b)
-        co_h = batch.cam_offs[3 * a:3 * b + 1] - batch.cam_offs[3 * a]
-        ch = {"first": a, "n": b - a, "co_h": co_h}
-        ch["pts"] = torch.from_numpy(batch.pts[batch.cam_offs[3 * a]:batch.cam_offs[3 * b]]).to(dev)
-        ch["cam_offs"] = torch.from_numpy(co_h).to(dev)
-        ch["F"] = torch.from_numpy(batch.F[3 * a:3 * b]).to(dev)
-        ch["proj"] = torch.from_numpy(np.ascontiguousarray(proj[a:b])).to(dev)
-        tp = ops.TripletPlan(co_h, b - a, device=dev)
-        c3 = tp.counts
-        ch["tplan"] = tp
-        if free:
-            if not ops.cube_free_scenes(c3).all():
-                raise SystemExit("c2match --cube free: a scene outside the candidate-list class")
-            ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
-            ch["cube"] = None
-            # --lsap-input blocks: no 8-row minima (the lists gather whole blocks)
-            ch["bm8"] = torch.empty(max(tp.n_bmin8, 1) if lsap_input == "bmin8" else 0,
-                                    dtype=torch.int16, device=dev)
-            ch["bm32"] = torch.empty(max(tp.n_bm32, 8), dtype=torch.int16, device=dev)
-        else:
-            ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
-            ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
-            ch["am"] = torch.empty(tp.n_rows, dtype=torch.int32, device=dev)
-            ch["mv"] = torch.empty(tp.n_rows, dtype=torch.float32, device=dev)
-            ch["offs"] = tp.cube_offs[:-1].contiguous()
-            # the cube kernel also writes its 8-row minima, which the assignment
-            # reduces instead of reading the cubes once more (--lsap-input cost: off)
-            ch["bm8"] = (torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
-                         if lsap_input == "bmin8" else None)
-        ch["used"] = None                   # event: the previous step's reads of the buffers
-        chunks.append(ch)
+    side = torch.cuda.Stream(dev) if (n_chunks > 1 or pipeline) else stream
 
-    def step(ev=None):
+    def make_chunks():
+        chunks = []
+        for a, b in zip(bounds[:-1], bounds[1:]):
+            a, b = int(a), int(b)
+            co_h = batch.cam_offs[3 * a:3 * b + 1] - batch.cam_offs[3 * a]
+            ch = {"first": a, "n": b - a, "co_h": co_h}
+            ch["pts"] = torch.from_numpy(batch.pts[batch.cam_offs[3 * a]:batch.cam_offs[3 * b]]).to(dev)
+            ch["cam_offs"] = torch.from_numpy(co_h).to(dev)
+            ch["F"] = torch.from_numpy(batch.F[3 * a:3 * b]).to(dev)
+            ch["proj"] = torch.from_numpy(np.ascontiguousarray(proj[a:b])).to(dev)
+            tp = ops.TripletPlan(co_h, b - a, device=dev)
+            c3 = tp.counts
+            ch["tplan"] = tp
+            if free:
+                if not ops.cube_free_scenes(c3).all():
+                    raise SystemExit("c2match --cube free: a scene outside the candidate-list class")
+                ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev, resid=True)
+                ch["cube"] = None
+                # --lsap-input blocks: no 8-row minima (the lists gather whole blocks)
+                ch["bm8"] = torch.empty(max(tp.n_bmin8, 1) if lsap_input == "bmin8" else 0,
+                                        dtype=torch.int16, device=dev)
+                ch["bm32"] = torch.empty(max(tp.n_bm32, 8), dtype=torch.int16, device=dev)
+            else:
+                ch["lplan"] = ops.LsapPlan(c3[:, 0] * c3[:, 1], c3[:, 2], device=dev)
+                ch["cube"] = torch.empty(tp.n_cube, dtype=torch.float32, device=dev)
+                ch["am"] = torch.empty(tp.n_rows, dtype=torch.int32, device=dev)
+                ch["mv"] = torch.empty(tp.n_rows, dtype=torch.float32, device=dev)
+                ch["offs"] = tp.cube_offs[:-1].contiguous()
+                # the cube kernel also writes its 8-row minima, which the assignment
+                # reduces instead of reading the cubes once more (--lsap-input cost: off)
+                ch["bm8"] = (torch.empty(max(tp.n_bmin8, 1), dtype=torch.int16, device=dev)
+                             if lsap_input == "bmin8" else None)
+            ch["used"] = None                   # event: the previous step's reads of the buffers
+            chunks.append(ch)
+        return chunks
+
+    sets = [make_chunks() for _ in range(2 if pipeline else 1)]
+
+    def step(ev=None, chunks=sets[0]):
         outs = []
         cube_done = []
         for k, ch in enumerate(chunks):
@@ -671,12 +681,15 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                 u.record(side)
                 ch["used"] = u
             outs.append((r, c, st) + tuple(res))
-        stream.wait_stream(side)
+        if not pipeline:
+            stream.wait_stream(side)
         return outs
 
-    for _ in range(warmup):
-        step()
+    for w_ in range(warmup):
+        step(chunks=sets[w_ % len(sets)])
+    stream.wait_stream(side)
     torch.cuda.synchronize(dev)
+    chunks = sets[0]
     evs = [[[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in chunks]
            for _ in range(steps)]
     env.barrier()
@@ -684,11 +697,13 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
     with ClockSampler(dev) as clocks:
         t_start = time.perf_counter()
         for s_ in range(steps):
-            outs = step(evs[s_])
+            outs = step(evs[s_], chunks=sets[s_ % len(sets)])
+        stream.wait_stream(side)
         torch.cuda.synchronize(dev)
         env.barrier()
         elapsed = time.perf_counter() - t_start
     elapsed = max_over_ranks(env, elapsed)
+    chunks = sets[(steps - 1) % len(sets)]              # the last step's buffers (parity)
     # kernel time per stage, summed over the chunks (they overlap across stages)
     stage = np.array([[sum(e[k][0].elapsed_time(e[k][1]) for k in range(n_chunks)),
                        sum(e[k][2].elapsed_time(e[k][3]) for k in range(n_chunks)),
@@ -842,6 +857,9 @@ def match_line(args, env, wl, kernel_options, *, steps, warmup, cube_mode="free"
                               "stream, each chunk's assignment + select on a second stream once "
                               "its cube is written" if n_chunks > 1 else "eager op calls, serial"),
                    "match_chunks": n_chunks,
+                   "pipeline": (("consecutive steps overlap: step t's assignment + select on a second "
+                                 "stream while step t + 1's minima run, two buffer sets")
+                                if pipeline else "off: each step's chain completes before the next starts"),
                    "parallelism": f"scene-sharded x{world}" if env.initialised else "single GPU"},
         "stages_ms": {("minima" if free else "cube"): cube_ms, "lsap": lsap_ms, "select_dlt": sel_ms,
                       "note": ("rank 0, HIP events on each stage's stream, summed over the chunks, "
@@ -912,6 +930,9 @@ def main():
                     help="mvm_options fields for the launches (include/mvmatch.h; e.g. "
                          "pairwise_row_groups=2): kernel-path choices that never change results, "
                          "for A/B runs of the line itself; recorded in config.kernel_options")
+    ap.add_argument("--match-pipeline", choices=["on", "off"], default="off",
+                    help="c2match: overlap consecutive steps (step t's assignment + select on a "
+                         "second stream while step t + 1's minima run; two buffer sets)")
     ap.add_argument("--match-chunks", type=int, default=1,
                     help="c2match: scenes per step in this many chunks, the assignment of one "
                          "overlapping the cube of the next on a second stream (1: serial, the "
@@ -1591,7 +1612,8 @@ def main():
         torch.cuda.empty_cache()
         t0 = time.perf_counter()
         nested, nested_ok = match_line(args, env, dict(WORKLOADS["c2match"]), None, steps=20, warmup=3,
-                                       cube_mode="free", cpu_seconds=min(args.cpu_seconds, 5.0))
+                                       cube_mode="free", cpu_seconds=min(args.cpu_seconds, 5.0),
+                                       pipeline=args.match_pipeline == "on")
         nested["wall_s"] = time.perf_counter() - t0
         nested["note"] = ("BASELINE configs[1]'s association (C2: 1,000 captures x 3 x 256, what "
                           "match_objects returns), run after this line's timed region on the same "
