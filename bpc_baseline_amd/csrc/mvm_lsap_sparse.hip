@@ -506,10 +506,14 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
     auto decode = [&](int b, int &jt) { return sp_div(b, bps, rbps, jt); };   // -> g, jt
     const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
     // the block (g * bps + jt) lane `lane` holds in its q-th key
+    // ext: lane l holds the kpl keys at kpl l .. kpl l + kpl - 1 (kpl = 32 when
+    // a row has 2,048 keys, fewer for smaller problems, so that every lane
+    // still holds keys and theta is taken over 64 lane minima)
+    const int kpl = ext ? (rowk + 63) >> 6 : 0;
     auto block_of = [&](int q) {
         if (!ext) return lane + 64 * q;
         int g;
-        const int jt = sp_div(32 * lane + q, npad, rnpad, g);
+        const int jt = sp_div(kpl * lane + q, npad, rnpad, g);
         return g * bps + jt;
     };
     const KT *bm = reinterpret_cast<const KT *>(ws + y.bm);
@@ -529,20 +533,28 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
         } else {
             // 16-bit keys h: the block's upper bound (h << 16) | 0xFFFF, +inf's
             // key for h = 0xFF80 (every entry +inf), 0xFFFF padding -> kMax
-            static_assert(kQ == 32 && sizeof(KT) == 4, "ext: 32 keys per lane");
-            const uint4 *r4 = reinterpret_cast<const uint4 *>(bm16 + s_u * rowk) + 4 * lane;
+            static_assert(kQ == 32 && sizeof(KT) == 4, "ext: at most 32 keys per lane");
             auto up = [](uint32_t h) -> KT {
                 return h == 0xFFFFu ? K::kMax : h >= 0xFF80u ? (KT)0xFF800000u : (KT)((h << 16) | 0xFFFFu);
             };
+            const uint16_t *row16 = bm16 + s_u * rowk;
+            if (kpl == 32) {                               // 2,048 keys: four 16-byte loads per lane
+                const uint4 *r4 = reinterpret_cast<const uint4 *>(row16) + 4 * lane;
 #pragma unroll
-            for (int v = 0; v < 4; ++v) {                  // rowk is a multiple of 16
-                const uint4 w = 32 * lane + 8 * v < rowk ? r4[v] : make_uint4(~0u, ~0u, ~0u, ~0u);
-                const uint32_t d[4] = {w.x, w.y, w.z, w.w};
+                for (int v = 0; v < 4; ++v) {
+                    const uint4 w = r4[v];
+                    const uint32_t d[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    k[8 * v + 2 * e] = up(d[e] & 0xFFFFu);
-                    k[8 * v + 2 * e + 1] = up(d[e] >> 16);
+                    for (int e = 0; e < 4; ++e) {
+                        k[8 * v + 2 * e] = up(d[e] & 0xFFFFu);
+                        k[8 * v + 2 * e + 1] = up(d[e] >> 16);
+                    }
                 }
+            } else {
+                const uint16_t *lp = row16 + kpl * lane;    // immediate offsets per key
+                const int nk = min(kpl, rowk - kpl * lane);  // this lane's keys (may be <= 0)
+#pragma unroll
+                for (int q = 0; q < kQ; ++q) k[q] = q < nk ? up(lp[q]) : K::kMax;
             }
         }
         KT lm = k[0];                                      // this lane's smallest block key

@@ -298,3 +298,20 @@ def test_match_captures_cube_free_equals_keep_cube(cuda, parts):
     free = ops.cube_free_scenes(counts)
     if len(parts) == 3:
         assert free.any() and not free.all()
+
+
+@pytest.mark.parametrize("n", [64, 100, 256])
+def test_resid_lists_hold_on_small_rows(cuda, n):
+    """Every lane of the list kernel holds block keys whatever a row's key
+    count (64^3 problems have 128 per row, 256^3 2,048), so theta stays the
+    16th-smallest of 64 lane minima and the lists do not overflow wholesale
+    (a 64^3 batch once overflowed every list and fell back to dense scans)."""
+    from bpc_baseline_amd import ops
+    counts = [(n, n, n)] * 8
+    plan, lres, _, _, (r1, c1, s1), (r0, c0, s0), _, _ = _assign_both(cuda, counts, 21)
+    assert (s1.cpu().numpy() == 0).all()
+    assert torch.equal(r1, r0) and torch.equal(c1, c0)
+    stats = ops.lsap_sparse_stats(lres)
+    rows = sum(c[2] for c in counts)
+    assert stats[:, 2].sum() <= 0.02 * rows, stats[:, 2]          # overflowed lists
+    assert stats[:, 0].sum() <= 0.05 * rows, stats[:, 0]          # dense free-minimum scans

@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=50)
+    ap.add_argument("--keep-cube", action="store_true",
+                    help="match_captures(keep_cube=True): the cube written and read (default: cube-free "
+                         "where the batch allows)")
     ap.add_argument("--rig-group", type=int, default=1,
                     help="consecutive captures sharing one camera rig (IPD: the images of a scene)")
     args = ap.parse_args()
@@ -59,11 +62,11 @@ def main():
     boxes, conf, cls, offs = t(b.boxes), t(b.conf), t(b.cls), t(b.img_offs)
     res = None
     for _ in range(args.warmup):
-        res = match_captures(boxes, conf, cls, offs, b.Ks, b.RTs)
+        res = match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, keep_cube=args.keep_cube)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        res = match_captures(boxes, conf, cls, offs, b.Ks, b.RTs)
+        res = match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, keep_cube=args.keep_cube)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     # a static rig: F and P computed once and passed in
@@ -74,7 +77,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, F=Fd, proj=Pd)
+        match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, F=Fd, proj=Pd, keep_cube=args.keep_cube)
     torch.cuda.synchronize()
     dt_cached = (time.perf_counter() - t0) / args.steps
     # the same batches through the pipelined stream (host F/P of batch b+1
@@ -102,7 +105,7 @@ def main():
         assert np.array_equal(ms[o:o + k], mr[o:o + k]), s
     stages = {}
     for _ in range(args.steps):
-        match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, timings=stages)
+        match_captures(boxes, conf, cls, offs, b.Ks, b.RTs, timings=stages, keep_cube=args.keep_cube)
     stages = {k: round(v / args.steps * 1e3, 3) for k, v in stages.items()}
 
     # parity spot-check on a few captures, then the CPU chain on a sample
@@ -123,7 +126,7 @@ def main():
     print(json.dumps({
         "metric": "captures matched/sec (detect-pack + cube + LSAP + select + DLT)",
         "value": args.captures / dt, "unit": "captures/s", "ms_per_batch": dt * 1e3,
-        "config": {"captures": args.captures, "dets_per_view": args.dets, "cams": 3,
+        "config": {"captures": args.captures, "dets_per_view": args.dets, "cams": 3, "keep_cube": args.keep_cube,
                    "captures_per_rig": args.rig_group},
         "matches": int(res.count.sum()), "parity_checked": len(check),
         "stage_ms_synchronised": stages,
