@@ -538,7 +538,9 @@ __global__ __launch_bounds__(kSpNT) void sp_lists_kernel(LsapSparseArgs a, int32
                 return h == 0xFFFFu ? K::kMax : h >= 0xFF80u ? (KT)0xFF800000u : (KT)((h << 16) | 0xFFFFu);
             };
             const uint16_t *row16 = bm16 + s_u * rowk;
-            if (kpl == 32) {                               // 2,048 keys: four 16-byte loads per lane
+            // kpl == 32 means rowk == 2,048 exactly (npad a multiple of 16, bps <= 8):
+            // four 16-byte loads per lane, all inside the row
+            if (kpl == 32) {
                 const uint4 *r4 = reinterpret_cast<const uint4 *>(row16) + 4 * lane;
 #pragma unroll
                 for (int v = 0; v < 4; ++v) {
