@@ -306,3 +306,29 @@ def test_bench_gpus_n_without_launcher(tmp_path, world):
     rows = n_scenes * 6 * 1024
     assert line["parity_rows"] == f"{rows}/{rows} bit-exact vs oracle"
     assert line["roofline"]["per_slot"]["slots"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cube,extra", [("free", []), ("free", ["--match-pipeline", "on"]),
+                                        ("free", ["--lsap-input", "bmin8"]), ("keep", [])])
+def test_bench_c2match_line_small(cube, extra):
+    """bench.py --workload c2match on a small batch: the line's own parity
+    against the CPU chain (block keys or cube, residuals, assignment, matches,
+    costs, X) holds in every mode, serial or with consecutive steps
+    overlapped, with and without the 8-row minima, with and without the cube."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("MVM_DIST_FORCE", None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--workload", "c2match",
+                        "--scenes", "24", "--steps", "3", "--warmup", "1", "--cpu-seconds", "0",
+                        "--cube", cube, *extra],
+                       env=env, capture_output=True, text=True, timeout=300, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["parity"].startswith("equal vs the CPU chain"), line["parity"]
+    assert all(all(v for k, v in d.items() if k != "scene" and k != "matches")
+               for d in line["parity_detail"]), line["parity_detail"]
+    assert line["value"] > 0 and line["config"]["n_scenes_total"] == 24
