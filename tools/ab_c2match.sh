@@ -13,6 +13,6 @@ for r in $(seq 1 "${2:-2}"); do
     opt=(); [ "$v" != default ] && opt=(--options "$v")
     timeout -k 10 400 python -u bench.py --workload c2match --steps 3 --warmup 1 --cpu-seconds 0 "${opt[@]}" \
       > "$O/$tag.$r.json" 2> "$O/$tag.$r.err" || { tail -5 "$O/$tag.$r.err"; exit 1; }
-    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], round(d['value']), round(d['stages_ms']['cube'],3), round(d['stages_ms']['lsap'],3), d['parity'])" "$O/$tag.$r.json" "$v"
+    python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); print(sys.argv[2], round(d['value']), round(d['stages_ms'].get('cube', d['stages_ms'].get('minima', 0)),3), round(d['stages_ms']['lsap'],3), d['parity'])" "$O/$tag.$r.json" "$v"
   done
 done
